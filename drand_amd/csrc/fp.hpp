@@ -1,0 +1,280 @@
+// BLS12-381 base field Fp on gfx950: 12 x 32-bit limbs, Montgomery form (R = 2^384).
+//
+// One field element lives in 12 VGPRs of one lane; every lane of a wave works on its own
+// beacon, so all arithmetic here is per-lane SIMT code with no cross-lane traffic.
+// Multiplication is CIOS with the "no final carry word" shortcut (p's top limb < 2^31),
+// written so that each partial product lowers to one v_mad_u64_u32.
+//
+// Replaces the Fp arithmetic of kilic/bls12-381 v0.1.0 (arithmetic_x86.s / fp.go) that
+// kyber-bls12381 v0.2.5 uses behind /root/reference/crypto/schemes.go:98,139,177.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "consts.hpp"
+
+namespace dh {
+
+#define DH_DEV __device__ __forceinline__
+
+struct fp {
+  uint32_t v[12];
+};
+
+// p, little-endian 32-bit limbs
+#define DH_P0 0xffffaaabu
+#define DH_P1 0xb9feffffu
+#define DH_P2 0xb153ffffu
+#define DH_P3 0x1eabfffeu
+#define DH_P4 0xf6b0f624u
+#define DH_P5 0x6730d2a0u
+#define DH_P6 0xf38512bfu
+#define DH_P7 0x64774b84u
+#define DH_P8 0x434bacd7u
+#define DH_P9 0x4b1ba7b6u
+#define DH_P10 0x397fe69au
+#define DH_P11 0x1a0111eau
+#define DH_NP0 0xfffcfffdu  // -p^-1 mod 2^32
+
+DH_DEV uint32_t p_limb(int i) {
+  switch (i) {
+    case 0: return DH_P0; case 1: return DH_P1; case 2: return DH_P2; case 3: return DH_P3;
+    case 4: return DH_P4; case 5: return DH_P5; case 6: return DH_P6; case 7: return DH_P7;
+    case 8: return DH_P8; case 9: return DH_P9; case 10: return DH_P10; default: return DH_P11;
+  }
+}
+
+DH_DEV fp fp_zero() {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = 0;
+  return r;
+}
+
+// R mod p (Montgomery one)
+DH_DEV fp fp_one() {
+  fp r;
+  r.v[0] = 0x0002fffdu; r.v[1] = 0x76090000u; r.v[2] = 0xc40c0002u; r.v[3] = 0xebf4000bu;
+  r.v[4] = 0x53c758bau; r.v[5] = 0x5f489857u; r.v[6] = 0x70525745u; r.v[7] = 0x77ce5853u;
+  r.v[8] = 0xa256ec6du; r.v[9] = 0x5c071a97u; r.v[10] = 0xfa80e493u; r.v[11] = 0x15f65ec3u;
+  return r;
+}
+
+// R^2 mod p (to enter Montgomery form)
+DH_DEV fp fp_r2() {
+  fp r;
+  r.v[0] = 0x1c341746u; r.v[1] = 0xf4df1f34u; r.v[2] = 0x09d104f1u; r.v[3] = 0x0a76e6a6u;
+  r.v[4] = 0x4c95b6d5u; r.v[5] = 0x8de5476cu; r.v[6] = 0x939d83c0u; r.v[7] = 0x67eb88a9u;
+  r.v[8] = 0xb519952du; r.v[9] = 0x9a793e85u; r.v[10] = 0x92cae3aau; r.v[11] = 0x11988fe5u;
+  return r;
+}
+
+// r = a - p if a >= p else a   (a < 2p)
+DH_DEV void fp_reduce_once(fp& a) {
+  uint32_t d[12];
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)a.v[i] - p_limb(i) - borrow;
+    d[i] = (uint32_t)t;
+    borrow = (t >> 63) & 1;
+  }
+  // borrow == 0  <=>  a >= p
+#pragma unroll
+  for (int i = 0; i < 12; i++) a.v[i] = borrow ? a.v[i] : d[i];
+}
+
+DH_DEV fp fp_add(const fp& a, const fp& b) {
+  fp r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)a.v[i] + b.v[i] + c;
+    r.v[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+  fp_reduce_once(r);  // a+b < 2p < 2^382, no limb overflow
+  return r;
+}
+
+DH_DEV fp fp_sub(const fp& a, const fp& b) {
+  fp r;
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)a.v[i] - b.v[i] - borrow;
+    r.v[i] = (uint32_t)t;
+    borrow = (t >> 63) & 1;
+  }
+  // if negative add p back
+  uint32_t mask = 0u - (uint32_t)borrow;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)r.v[i] + (p_limb(i) & mask) + c;
+    r.v[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+  return r;
+}
+
+DH_DEV fp fp_neg(const fp& a) {
+  // p - a, and 0 -> 0
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) nz |= a.v[i];
+  uint32_t mask = nz ? 0xffffffffu : 0u;
+  fp r;
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)(p_limb(i) & mask) - a.v[i] - borrow;
+    r.v[i] = (uint32_t)t;
+    borrow = (t >> 63) & 1;
+  }
+  return r;
+}
+
+DH_DEV fp fp_dbl(const fp& a) { return fp_add(a, a); }
+
+DH_DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  return (uint64_t)a * (uint64_t)b + c;
+}
+
+// Montgomery product a*b*R^-1 mod p, inputs < p, output < p.
+DH_DEV fp fp_mul(const fp& a, const fp& b) {
+  uint32_t t[12];
+#pragma unroll
+  for (int j = 0; j < 12; j++) t[j] = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint32_t bi = b.v[i];
+    uint64_t A = mad64(a.v[0], bi, t[0]);
+    t[0] = (uint32_t)A;
+    const uint32_t m = t[0] * DH_NP0;
+    uint64_t C = mad64(m, DH_P0, t[0]);
+#pragma unroll
+    for (int j = 1; j < 12; j++) {
+      A = mad64(a.v[j], bi, (uint64_t)t[j] + (A >> 32));
+      t[j] = (uint32_t)A;
+      C = mad64(m, p_limb(j), (uint64_t)t[j] + (C >> 32));
+      t[j - 1] = (uint32_t)C;
+    }
+    t[11] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+  }
+  fp r;
+#pragma unroll
+  for (int j = 0; j < 12; j++) r.v[j] = t[j];
+  fp_reduce_once(r);
+  return r;
+}
+
+DH_DEV fp fp_sqr(const fp& a) { return fp_mul(a, a); }
+
+DH_DEV bool fp_is_zero(const fp& a) {
+  uint32_t nz = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) nz |= a.v[i];
+  return nz == 0;
+}
+
+DH_DEV bool fp_eq(const fp& a, const fp& b) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) d |= a.v[i] ^ b.v[i];
+  return d == 0;
+}
+
+DH_DEV fp fp_select(bool c, const fp& a, const fp& b) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+DH_DEV fp fp_to_mont(const fp& a) { return fp_mul(a, fp_r2()); }
+
+DH_DEV fp fp_from_mont(const fp& a) {
+  fp one = fp_zero();
+  one.v[0] = 1;
+  return fp_mul(a, one);
+}
+
+// load a constant-memory Montgomery element
+DH_DEV fp fp_c(const uint32_t* c) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = c[i];
+  return r;
+}
+
+DH_DEV fp fp_mul_c(const fp& a, const uint32_t* c) { return fp_mul(a, fp_c(c)); }
+
+// x^e for a public exponent held as little-endian 32-bit words (uniform across lanes, so
+// the multiply branch is a scalar branch: no divergence).
+DH_DEV fp fp_pow_words(const fp& x, const uint32_t* e, int nbits) {
+  fp acc = x;  // top bit is 1
+  for (int b = nbits - 2; b >= 0; b--) {
+    acc = fp_sqr(acc);
+    if ((e[b >> 5] >> (b & 31)) & 1) acc = fp_mul(acc, x);
+  }
+  return acc;
+}
+
+DH_DEV fp fp_inv(const fp& x) { return fp_pow_words(x, cst::EXP_P_MINUS_2, cst::EXP_P_MINUS_2_BITS); }
+
+// returns true and r = sqrt(a) if a is a square
+DH_DEV bool fp_sqrt(fp& r, const fp& a) {
+  r = fp_pow_words(a, cst::EXP_P_PLUS_1_DIV_4, cst::EXP_P_PLUS_1_DIV_4_BITS);
+  return fp_eq(fp_sqr(r), a);
+}
+
+// canonical (non-Montgomery) integer comparison helpers
+DH_DEV bool int_gt_half_p(const fp& canon) {
+  // (p-1)/2 limbs
+  const uint32_t h[12] = {0xffffd555u, 0xdcff7fffu, 0x58a9ffffu, 0x0f55ffffu, 0x7b587b12u, 0xb3986950u,
+                          0x79c2895fu, 0xb23ba5c2u, 0x21a5d66bu, 0x258dd3dbu, 0x1cbff34du, 0x0d0088f5u};
+  // canon > h ?
+  bool gt = false, decided = false;
+#pragma unroll
+  for (int i = 11; i >= 0; i--) {
+    bool g = canon.v[i] > h[i], l = canon.v[i] < h[i];
+    gt = decided ? gt : g;
+    decided = decided || g || l;
+  }
+  return gt;
+}
+
+DH_DEV bool int_lt_p(const uint32_t* x) {
+  bool lt = false, decided = false;
+#pragma unroll
+  for (int i = 11; i >= 0; i--) {
+    uint32_t pl = p_limb(i);
+    bool l = x[i] < pl, g = x[i] > pl;
+    lt = decided ? lt : l;
+    decided = decided || g || l;
+  }
+  return lt;
+}
+
+// RFC 9380 sgn0 for Fp: parity of the canonical value
+DH_DEV uint32_t fp_sgn0(const fp& a) { return fp_from_mont(a).v[0] & 1; }
+
+// 48 big-endian bytes (top 3 bits masked by the caller) -> limbs (no reduction)
+DH_DEV void be48_to_limbs(uint32_t* out, const uint8_t* in) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint8_t* q = in + 44 - 4 * i;
+    out[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+
+DH_DEV void limbs_to_be48(uint8_t* out, const fp& canon) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint8_t* q = out + 44 - 4 * i;
+    uint32_t v = canon.v[i];
+    q[0] = v >> 24; q[1] = v >> 16; q[2] = v >> 8; q[3] = v;
+  }
+}
+
+}  // namespace dh

@@ -1,0 +1,119 @@
+// Fp2 = Fp[i]/(i^2 + 1) on gfx950 (per-lane, 24 VGPRs per element).
+// Replaces kilic/bls12-381 v0.1.0 fp2.go as used for G2 signatures / keys
+// (/root/reference/crypto/schemes.go:99-101,140-142,178-180).
+#pragma once
+#include "fp.hpp"
+
+namespace dh {
+
+struct fp2 {
+  fp c0, c1;
+};
+
+DH_DEV fp2 fp2_zero() { return {fp_zero(), fp_zero()}; }
+DH_DEV fp2 fp2_one() { return {fp_one(), fp_zero()}; }
+DH_DEV fp2 fp2_c(const uint32_t (*c)[12]) { return {fp_c(c[0]), fp_c(c[1])}; }
+DH_DEV fp2 fp2_add(const fp2& a, const fp2& b) { return {fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+DH_DEV fp2 fp2_sub(const fp2& a, const fp2& b) { return {fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+DH_DEV fp2 fp2_dbl(const fp2& a) { return {fp_dbl(a.c0), fp_dbl(a.c1)}; }
+DH_DEV fp2 fp2_neg(const fp2& a) { return {fp_neg(a.c0), fp_neg(a.c1)}; }
+DH_DEV fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }
+
+// Karatsuba: 3 Fp products
+DH_DEV fp2 fp2_mul(const fp2& a, const fp2& b) {
+  fp t0 = fp_mul(a.c0, b.c0);
+  fp t1 = fp_mul(a.c1, b.c1);
+  fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
+}
+
+// complex squaring: 2 Fp products
+DH_DEV fp2 fp2_sqr(const fp2& a) {
+  fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  fp t1 = fp_mul(a.c0, a.c1);
+  return {t0, fp_dbl(t1)};
+}
+
+DH_DEV fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
+
+// multiply by the Fp6 non-residue xi = 1 + i
+DH_DEV fp2 fp2_mul_xi(const fp2& a) { return {fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+DH_DEV bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+DH_DEV bool fp2_eq(const fp2& a, const fp2& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+DH_DEV fp2 fp2_select(bool c, const fp2& a, const fp2& b) { return {fp_select(c, a.c0, b.c0), fp_select(c, a.c1, b.c1)}; }
+
+DH_DEV fp2 fp2_inv(const fp2& a) {
+  fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp ni = fp_inv(n);
+  return {fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
+}
+
+DH_DEV fp2 fp2_pow_words(const fp2& x, const uint32_t* e, int nbits) {
+  fp2 acc = x;
+  for (int b = nbits - 2; b >= 0; b--) {
+    acc = fp2_sqr(acc);
+    if ((e[b >> 5] >> (b & 31)) & 1) acc = fp2_mul(acc, x);
+  }
+  return acc;
+}
+
+DH_DEV fp2 fp2_pow_small(const fp2& x, uint32_t e) {
+  fp2 acc = fp2_one();
+  for (int b = 31; b >= 0; b--) {
+    acc = fp2_sqr(acc);
+    if ((e >> b) & 1) acc = fp2_mul(acc, x);
+  }
+  return acc;
+}
+
+// RFC 9380 sgn0 for Fp2
+DH_DEV uint32_t fp2_sgn0(const fp2& a) {
+  fp c0 = fp_from_mont(a.c0), c1 = fp_from_mont(a.c1);
+  uint32_t s0 = c0.v[0] & 1, s1 = c1.v[0] & 1;
+  uint32_t z0 = fp_is_zero(c0) ? 1u : 0u;
+  return s0 | (z0 & s1);
+}
+
+// RFC 9380 Appendix F.2.1.1 sqrt_ratio (generic, here c1 = 3 for q = p^2).
+// Returns isQR; y = sqrt(u/v) if QR else sqrt(Z*u/v).
+DH_DEV bool fp2_sqrt_ratio(fp2& y, const fp2& u, const fp2& v) {
+  fp2 tv1 = fp2_c(cst::SQRT_RATIO2_C6);
+  fp2 tv2 = fp2_pow_small(v, cst::SR2_C4);
+  fp2 tv3 = fp2_mul(fp2_sqr(tv2), v);
+  fp2 tv5 = fp2_mul(u, tv3);
+  tv5 = fp2_pow_words(tv5, cst::EXP_SR2_C3, cst::EXP_SR2_C3_BITS);
+  tv5 = fp2_mul(tv5, tv2);
+  tv2 = fp2_mul(tv5, v);
+  tv3 = fp2_mul(tv5, u);
+  fp2 tv4 = fp2_mul(tv3, tv2);
+  tv5 = fp2_pow_small(tv4, cst::SR2_C5);
+  bool isQR = fp2_eq(tv5, fp2_one());
+  tv2 = fp2_mul(tv3, fp2_c(cst::SQRT_RATIO2_C7));
+  tv5 = fp2_mul(tv4, tv1);
+  tv3 = fp2_select(isQR, tv3, tv2);
+  tv4 = fp2_select(isQR, tv4, tv5);
+#pragma unroll
+  for (int i = cst::SR2_C1; i >= 2; i--) {
+    tv5 = tv4;
+    for (int k = 0; k < i - 2; k++) tv5 = fp2_sqr(tv5);
+    bool e1 = fp2_eq(tv5, fp2_one());
+    tv2 = fp2_mul(tv3, tv1);
+    tv1 = fp2_sqr(tv1);
+    tv5 = fp2_mul(tv4, tv1);
+    tv3 = fp2_select(e1, tv3, tv2);
+    tv4 = fp2_select(e1, tv4, tv5);
+  }
+  y = tv3;
+  return isQR;
+}
+
+// square root in Fp2 (any root); false if a is not a square
+DH_DEV bool fp2_sqrt(fp2& r, const fp2& a) {
+  fp2 y;
+  bool qr = fp2_sqrt_ratio(y, a, fp2_one());
+  r = y;
+  return qr && fp2_eq(fp2_sqr(y), a);
+}
+
+}  // namespace dh
