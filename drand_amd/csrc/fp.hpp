@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "consts.hpp"
+#include "fp_mul_fips.hpp"
 
 namespace dh {
 
@@ -140,8 +141,8 @@ DH_DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   return (uint64_t)a * (uint64_t)b + c;
 }
 
-// Montgomery product a*b*R^-1 mod p, inputs < p, output < p.
-DH_DEV fp fp_mul(const fp& a, const fp& b) {
+// Textbook CIOS Montgomery product (kept as the microbenchmark baseline, bench/microbench_fp.hip).
+DH_DEV fp fp_mul_cios(const fp& a, const fp& b) {
   uint32_t t[12];
 #pragma unroll
   for (int j = 0; j < 12; j++) t[j] = 0;
@@ -168,7 +169,64 @@ DH_DEV fp fp_mul(const fp& a, const fp& b) {
   return r;
 }
 
-DH_DEV fp fp_sqr(const fp& a) { return fp_mul(a, a); }
+// The field product used everywhere: product-scanning Montgomery (fp_mul_fips.hpp), called through
+// an out-of-line function with a register-passing vector ABI so that the large kernels (pairing,
+// hash-to-curve) stay compact; define DH_MUL_INLINE to inline it instead.
+typedef uint32_t fpvec __attribute__((ext_vector_type(12)));
+
+__device__ __noinline__ fpvec fp_mul_vec(fpvec a, fpvec b) {
+  uint32_t x[12], y[12], r[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) { x[i] = a[i]; y[i] = b[i]; }
+  fips_mont_mul(r, x, y);
+  fpvec o;
+#pragma unroll
+  for (int i = 0; i < 12; i++) o[i] = r[i];
+  return o;
+}
+__device__ __noinline__ fpvec fp_sqr_vec(fpvec a) {
+  uint32_t x[12], r[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) x[i] = a[i];
+  fips_mont_sqr(r, x);
+  fpvec o;
+#pragma unroll
+  for (int i = 0; i < 12; i++) o[i] = r[i];
+  return o;
+}
+DH_DEV fpvec to_vec(const fp& a) {
+  fpvec v;
+#pragma unroll
+  for (int i = 0; i < 12; i++) v[i] = a.v[i];
+  return v;
+}
+DH_DEV fp from_vec(const fpvec& v) {
+  fp a;
+#pragma unroll
+  for (int i = 0; i < 12; i++) a.v[i] = v[i];
+  return a;
+}
+
+DH_DEV fp fp_mul(const fp& a, const fp& b) {
+#ifdef DH_MUL_INLINE
+  fp r;
+  fips_mont_mul(r.v, a.v, b.v);
+  return r;
+#else
+  return from_vec(fp_mul_vec(to_vec(a), to_vec(b)));
+#endif
+}
+
+DH_DEV fp fp_sqr(const fp& a) {
+#ifdef DH_MUL_INLINE
+  fp r;
+  fips_mont_sqr(r.v, a.v);
+  return r;
+#else
+  return from_vec(fp_sqr_vec(to_vec(a)));
+#endif
+}
+
 
 DH_DEV bool fp_is_zero(const fp& a) {
   uint32_t nz = 0;

@@ -1,0 +1,53 @@
+// Host-side declarations of the kernel launchers in kernels.hip (internal to libdrandhip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace dh {
+
+// Pippenger geometry for one MSM level: entries are cut into groups of `gsize` consecutive entries;
+// each group has nwin windows of c bits (128-bit scalars) with nbuck = 2^c buckets (digit 0 unused);
+// bucket reduction splits the digits of a window into nseg segments of seglen digits.
+struct msm_geom {
+  uint32_t gsize;
+  int c;
+  int nwin;
+  uint32_t nbuck;
+  uint32_t nseg;
+  uint32_t seglen;
+};
+
+// device workspace of one MSM level (sized by the caller from msm_geom)
+struct msm_ws {
+  uint32_t* cnt;       // nkeys
+  uint32_t* off;       // nkeys + 1
+  uint32_t* scan_tmp;  // ceil(nkeys / 4096)
+  uint32_t* list;      // m * nwin
+  uint32_t* buckets;   // nkeys Jacobian points
+  uint32_t* segs;      // ngroups * nwin * nseg Jacobian points
+};
+
+hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n, uint8_t* status, uint32_t* sig_aff,
+                       uint8_t* rand_out, hipStream_t st);
+hipError_t launch_msg(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
+                      size_t n, int chained, int dst_id, uint32_t* q_out, hipStream_t st);
+hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, hipStream_t st);
+hipError_t launch_decode_key(int key_g2, const uint8_t* pk, uint32_t* key_aff, uint8_t* ok, hipStream_t st);
+hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t st);
+hipError_t launch_scan(const uint32_t* cnt, size_t nk, uint32_t* off, uint32_t* tmp, hipStream_t st);
+hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
+                      const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
+                      hipStream_t st);
+hipError_t launch_group_check(int sig_g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_aff,
+                              uint8_t* pass, hipStream_t st);
+hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,
+                              uint8_t* verdict, hipStream_t st);
+hipError_t launch_leaf_check(int sig_g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
+                             const uint32_t* key_aff, const uint8_t* status, uint8_t* verdict, hipStream_t st);
+
+hipError_t launch_sign(int sig_g2, const uint32_t* sk, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride,
+                       const uint32_t* prev_lens, size_t n, int chained, int dst_id, uint8_t* out, hipStream_t st);
+hipError_t launch_pubkey(int key_g2, const uint32_t* sk, uint8_t* out, hipStream_t st);
+
+}  // namespace dh

@@ -1,0 +1,178 @@
+"""Host mirror of drand's crypto.Scheme over libdrandhip (the gfx950 verification engine).
+
+Mirrors /root/reference/crypto/schemes.go:
+  Scheme (fields Name / sig & key group sizes)           schemes.go:46-67
+  Scheme.VerifyBeacon(beacon, pubkey) -> error (raise)    schemes.go:70-72
+  Scheme.DigestBeacon                                     schemes.go:106-114 (chained), 147-151, 187-191
+  SchemeFromName / ListSchemes / GetSchemeByIDWithDefault schemes.go:206-235
+  GetSchemeFromEnv (SCHEME_ID)                            schemes.go:239-243
+plus the batch entry point the reference lacks (Scheme.verify_beacons) and the RFC 9380 quicknet
+scheme "bls-unchained-g1-rfc9380", which this snapshot of the reference does not have.
+
+Errors follow the Go shape: VerifyBeacon raises SchemeError for an invalid beacon (Go returns a
+non-nil error); batch calls return per-round booleans. Device failures raise DeviceError, never fall
+back to a CPU path.
+"""
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+DEFAULT_SCHEME = "pedersen-bls-chained"        # DefaultSchemeID
+UNCHAINED_SCHEME = "pedersen-bls-unchained"    # UnchainedSchemeID
+SHORT_SIG_SCHEME = "bls-unchained-on-g1"       # ShortSigSchemeID
+SIGS_ON_G1_SCHEME = "bls-unchained-g1-rfc9380"  # quicknet (RFC 9380 G1 DST); absent from the reference snapshot
+
+_IDS = {DEFAULT_SCHEME: 0, UNCHAINED_SCHEME: 1, SHORT_SIG_SCHEME: 2, SIGS_ON_G1_SCHEME: 3}
+
+
+class SchemeError(ValueError):
+    """A verification / decoding failure (the Go API's non-nil error)."""
+
+
+class DeviceError(RuntimeError):
+    """libdrandhip reported a device / runtime failure."""
+
+
+def _check(rc):
+    if rc >= 0:
+        return rc
+    msg = _lib.last_error()
+    if rc in (_lib.DH_EINVAL, _lib.DH_EKEY, _lib.DH_ERECOVER):
+        raise SchemeError(msg)
+    raise DeviceError("libdrandhip error %d: %s" % (rc, msg))
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+@dataclass(frozen=True)
+class Scheme:
+    name: str
+    id: int
+    sig_len: int   # SigGroup point length (compressed)
+    key_len: int   # KeyGroup point length
+    chained: bool
+
+    # ---- reference-shaped single-beacon API
+    def digest_beacon(self, round_, previous_signature=b""):
+        """crypto.Scheme.DigestBeacon: SHA-256(prev || round_be64) (chained) or SHA-256(round_be64)."""
+        out = np.zeros(32, dtype=np.uint8)
+        rounds = np.array([round_], dtype=np.uint64)
+        prev = np.frombuffer(bytes(previous_signature), dtype=np.uint8).copy() if self.chained else None
+        plen = np.array([len(previous_signature)], dtype=np.uint32) if self.chained else None
+        _check(_lib.load().dh_digest_batch(self.id, _ptr(rounds), _ptr(prev) if prev is not None and len(prev) else None,
+                                           max(1, len(previous_signature)), _ptr(plen), 1, _ptr(out)))
+        return out.tobytes()
+
+    def verify_beacon(self, beacon, pubkey):
+        """crypto.Scheme.VerifyBeacon: raises SchemeError if the beacon does not verify."""
+        prev = bytes(beacon.previous_signature or b"") if self.chained else b""
+        rc = _lib.load().dh_verify_beacon(self.id, bytes(pubkey), len(pubkey), int(beacon.round),
+                                          bytes(beacon.signature), len(beacon.signature), prev, len(prev))
+        if _check(rc) != 1:
+            raise SchemeError("bls: invalid signature")
+
+    # ---- batch API (new): one call for many rounds sharing the group key
+    def verify_beacons(self, pubkey, rounds, signatures, previous_signatures=None, seed=0, want_randomness=True):
+        """Verify n rounds at once.
+
+        rounds: (n,) uint64; signatures: (n, sig_len) uint8; previous_signatures (chained only):
+        (n, L) uint8 with L a multiple of 4 <= 96, or a list of bytes (lengths may differ).
+        Returns (verdicts (n,) bool, randomness (n, 32) uint8 or None)."""
+        rounds = np.ascontiguousarray(rounds, dtype=np.uint64)
+        sigs = np.ascontiguousarray(signatures, dtype=np.uint8)
+        n = len(rounds)
+        if sigs.shape != (n, self.sig_len):
+            raise SchemeError("signatures must be (%d, %d)" % (n, self.sig_len))
+        prev = plen = None
+        pstride = 0
+        if self.chained and previous_signatures is not None:
+            prev, plen, pstride = _pack_prevs(previous_signatures, n)
+        verdict = np.zeros(n, dtype=np.uint8)
+        rand = np.zeros((n, 32), dtype=np.uint8) if want_randomness else None
+        _check(_lib.load().dh_verify_batch(self.id, bytes(pubkey), len(pubkey), _ptr(rounds), _ptr(sigs), self.sig_len,
+                                           _ptr(prev), pstride, _ptr(plen), n, _ptr(verdict), _ptr(rand), int(seed)))
+        return verdict.astype(bool), rand
+
+    def randomness(self, signatures):
+        sigs = np.ascontiguousarray(signatures, dtype=np.uint8)
+        out = np.zeros((len(sigs), 32), dtype=np.uint8)
+        _check(_lib.load().dh_randomness_batch(self.id, _ptr(sigs), self.sig_len, len(sigs), _ptr(out)))
+        return out
+
+    # ---- synthetic-chain utilities (tests / bench): device signer
+    def sign_beacons(self, secret32, rounds, previous_signatures=None):
+        rounds = np.ascontiguousarray(rounds, dtype=np.uint64)
+        n = len(rounds)
+        prev = plen = None
+        pstride = 0
+        if self.chained and previous_signatures is not None:
+            prev, plen, pstride = _pack_prevs(previous_signatures, n)
+        out = np.zeros((n, self.sig_len), dtype=np.uint8)
+        _check(_lib.load().dh_sign_batch(self.id, bytes(secret32), _ptr(rounds), _ptr(prev), n if prev is None else n,
+                                         _ptr(plen) if plen is not None else None, pstride, _ptr(out)))
+        return out
+
+    def public_key(self, secret32):
+        out = np.zeros(self.key_len, dtype=np.uint8)
+        _check(_lib.load().dh_public_key(self.id, bytes(secret32), _ptr(out)))
+        return out.tobytes()
+
+    def __str__(self):
+        return self.name
+
+
+def _pack_prevs(previous_signatures, n):
+    if isinstance(previous_signatures, np.ndarray) and previous_signatures.ndim == 2:
+        prev = np.ascontiguousarray(previous_signatures, dtype=np.uint8)
+        if len(prev) != n:
+            raise SchemeError("previous_signatures must have one row per round")
+        width = prev.shape[1]
+        if width % 4 or width > 96:
+            raise SchemeError("previous signature length must be a multiple of 4 and <= 96")
+        plen = np.full(n, width, dtype=np.uint32)
+        return prev, plen, max(width, 4)
+    items = [bytes(p or b"") for p in previous_signatures]
+    if len(items) != n:
+        raise SchemeError("previous_signatures must have one entry per round")
+    prev = np.zeros((n, 96), dtype=np.uint8)
+    plen = np.zeros(n, dtype=np.uint32)
+    for i, p in enumerate(items):
+        if len(p) % 4 or len(p) > 96:
+            raise SchemeError("previous signature %d has unsupported length %d" % (i, len(p)))
+        prev[i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
+        plen[i] = len(p)
+    return prev, plen, 96
+
+
+_SCHEMES = {
+    DEFAULT_SCHEME: Scheme(DEFAULT_SCHEME, 0, 96, 48, True),
+    UNCHAINED_SCHEME: Scheme(UNCHAINED_SCHEME, 1, 96, 48, False),
+    SHORT_SIG_SCHEME: Scheme(SHORT_SIG_SCHEME, 2, 48, 96, False),
+    SIGS_ON_G1_SCHEME: Scheme(SIGS_ON_G1_SCHEME, 3, 48, 96, False),
+}
+
+
+def scheme_from_name(name):
+    """crypto.SchemeFromName; raises SchemeError("invalid scheme name '...'")."""
+    try:
+        return _SCHEMES[name]
+    except KeyError:
+        raise SchemeError("invalid scheme name '%s'" % name) from None
+
+
+def list_schemes():
+    return list(_SCHEMES)
+
+
+def get_scheme_by_id_with_default(id_):
+    return scheme_from_name(id_ or DEFAULT_SCHEME)
+
+
+def get_scheme_from_env():
+    return get_scheme_by_id_with_default(os.environ.get("SCHEME_ID", ""))

@@ -157,6 +157,55 @@ def c_exp_words(e):
     return n, "{" + ", ".join("0x%08xu" % ((e >> (32 * i)) & 0xFFFFFFFF) for i in range(n)) + "}"
 
 
+DST_G2 = b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"
+DST_G1 = b"BLS_SIG_BLS12381G1_XMD:SHA-256_SSWU_RO_NUL_"
+SHA_IV = [0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19]
+SHA_K = [
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5, 0xd807aa98,
+    0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786,
+    0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8,
+    0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13,
+    0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819,
+    0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a,
+    0x5b9cca4f, 0x682e6ff3, 0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+    0xc67178f2]
+
+
+def _ror(x, n):
+    return ((x >> n) | (x << (32 - n))) & 0xFFFFFFFF
+
+
+def sha_compress(h, block):
+    wd = [int.from_bytes(block[4 * i:4 * i + 4], "big") for i in range(16)]
+    for i in range(16, 64):
+        s0 = _ror(wd[i - 15], 7) ^ _ror(wd[i - 15], 18) ^ (wd[i - 15] >> 3)
+        s1 = _ror(wd[i - 2], 17) ^ _ror(wd[i - 2], 19) ^ (wd[i - 2] >> 10)
+        wd.append((wd[i - 16] + s0 + wd[i - 7] + s1) & 0xFFFFFFFF)
+    a, b, c, d, e, f, g, hh = h
+    for i in range(64):
+        t1 = (hh + (_ror(e, 6) ^ _ror(e, 11) ^ _ror(e, 25)) + ((e & f) ^ (~e & g)) + SHA_K[i] + wd[i]) & 0xFFFFFFFF
+        t2 = ((_ror(a, 2) ^ _ror(a, 13) ^ _ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c))) & 0xFFFFFFFF
+        hh, g, f, e, d, c, b, a = g, f, e, (d + t1) & 0xFFFFFFFF, c, b, a, (t1 + t2) & 0xFFFFFFFF
+    return [(x + y) & 0xFFFFFFFF for x, y in zip(h, [a, b, c, d, e, f, g, hh])]
+
+
+def sha_pad(m, prefix_len):
+    """SHA-256 padding of m, which follows prefix_len already-compressed bytes."""
+    total = prefix_len + len(m)
+    m = m + b"\x80"
+    while (prefix_len + len(m)) % 64 != 56:
+        m += b"\x00"
+    return m + (8 * total).to_bytes(8, "big")
+
+
+def words(b):
+    return [int.from_bytes(b[4 * i:4 * i + 4], "big") for i in range(len(b) // 4)]
+
+
+def cw(ws):
+    return "{" + ", ".join("0x%08xu" % v for v in ws) + "}"
+
+
 def main():
     assert (P - 1) % 3 == 0 and P % 4 == 3
     xi = (1, 1)
@@ -234,6 +283,8 @@ def main():
     fp2_const("SQRT_RATIO2_C6", c6)
     fp2_const("SQRT_RATIO2_C7", c7)
     fp_const("K256", k256)
+    fp_const("K256R", k256 * MONT % P)  # mont_mul(raw hi, K256R) = Mont(hi * 2^256)
+    fp_const("R2", MONT % P)  # c_fp(R) = R^2 mod p: mont_mul(raw x, R2) = Mont(x)
     for name, txt in (("ISO11_XNUM", ISO11_XNUM), ("ISO11_XDEN", ISO11_XDEN), ("ISO11_YNUM", ISO11_YNUM),
                       ("ISO11_YDEN", ISO11_YDEN)):
         cs = [int(t, 16) for t in txt.split()]
@@ -255,8 +306,44 @@ def main():
     w("constexpr int SR2_C1 = %d;" % c1)
     w("constexpr uint64_t U_ABS = 0x%016xull;" % (-U))
     w("constexpr uint64_t H_EFF_G1 = 0x%016xull;" % h_eff_g1)
+    # G2 effective cofactor (RFC 9380 8.8.2), applied once per batch to the RLC sum of SSWU points
+    h_eff_g2 = 0xbc69f08f2ee75b3584c6a0ea91b352888e2a8e9145ad7689986ff031508ffe1329c2f178731db956d82bf015d1212b02ec0ec69d7477c1ae954cbc06689f6a359894c0adebbf6b4e8020005aaa95551
+    n, txt = c_exp_words(h_eff_g2)
+    w("constexpr int H_EFF_G2_WORDS = %d;" % n)
+    w("constexpr int H_EFF_G2_BITS = %d;" % h_eff_g2.bit_length())
+    w("__device__ __constant__ uint32_t H_EFF_G2[%d] = %s;" % (n, txt))
+    # G1 subgroup check / Miller loop parameter |u| as words
+    w("__device__ __constant__ uint32_t U_ABS_W[2] = {0x%08xu, 0x%08xu};" % ((-U) & 0xFFFFFFFF, (-U) >> 32))
     # scalar field r (8 x 32-bit limbs, plain) for tbls Lagrange
     w("__device__ __constant__ uint32_t R_LIMBS[8] = {%s};" % ", ".join("0x%08xu" % ((R >> (32 * i)) & 0xFFFFFFFF) for i in range(8)))
+    # ---- expand_message_xmd(SHA-256) block templates for a 32-byte message (the beacon digest).
+    # Byte layouts (RFC 9380 5.3.1): b0 = H(Z_pad || msg || I2OSP(len,2) || 0 || DST || len(DST)),
+    # b_i = H((b0 ^ b_{i-1}) || I2OSP(i,1) || DST || len(DST)). Message-dependent words are zero here
+    # and OR-ed in on the device.
+    for dname, dst in (("G2", DST_G2), ("G1", DST_G1)):
+        assert len(dst) == 43
+    w("constexpr int XMD_DST_LEN = 43;")
+    w("__device__ __constant__ uint32_t XMD_ZPAD_H[8] = {%s};" % ", ".join("0x%08xu" % v for v in sha_compress(SHA_IV, bytes(64))))
+    b0a, b0b, bia, bib = [], [], [], []
+    for dst in (DST_G2, DST_G1):
+        dstp = dst + bytes([len(dst)])
+        per_len = []
+        for L in (128, 256):
+            m = bytes(32) + L.to_bytes(2, "big") + b"\x00" + dstp
+            blocks = sha_pad(m, 64)
+            assert len(blocks) == 128
+            per_len.append(words(blocks[:64])[8:16])
+        b0a.append(per_len)
+        b0b.append(words(blocks[64:128]))
+        m = bytes(32) + b"\x00" + dstp
+        blocks = sha_pad(m, 0)
+        assert len(blocks) == 128
+        bia.append(words(blocks[:64])[8:16])
+        bib.append(words(blocks[64:128]))
+    w("__device__ __constant__ uint32_t XMD_B0A[2][2][8] = {%s};" % ", ".join("{" + ", ".join(cw(x) for x in pl) + "}" for pl in b0a))
+    w("__device__ __constant__ uint32_t XMD_B0B[2][16] = {%s};" % ", ".join(cw(x) for x in b0b))
+    w("__device__ __constant__ uint32_t XMD_BIA[2][8] = {%s};" % ", ".join(cw(x) for x in bia))
+    w("__device__ __constant__ uint32_t XMD_BIB[2][16] = {%s};" % ", ".join(cw(x) for x in bib))
     w("}  // namespace cst")
     w("}  // namespace dh")
     path = os.path.join(os.path.dirname(__file__), "..", "csrc", "consts.hpp")

@@ -1,0 +1,130 @@
+/*
+ * drandhip.h — C ABI of libdrandhip, the MI355X (gfx950) beacon-verification engine for drand.
+ *
+ * Plain pointers and sizes only (cgo / ctypes / JNI friendly). Every entry point is thread-safe and
+ * reentrant: concurrent callers each get their own HIP stream and device workspace from an internal
+ * pool. Inputs are borrowed for the duration of the call and never retained; outputs are written into
+ * caller-owned buffers. Batch calls block until their results are on the host.
+ *
+ * Replaces, for the verification hot path, the kyber / kyber-bls12381 / kilic arithmetic that drand
+ * reaches through (reference at /root/reference, drand snapshot 2025-01-17):
+ *   crypto.Scheme.VerifyBeacon            crypto/schemes.go:70-72
+ *   crypto.Scheme.DigestBeacon            crypto/schemes.go:106-114 (chained), 147-151, 187-191
+ *   crypto.RandomnessFromSignature        crypto/schemes.go:249-252
+ *   crypto.SchemeFromName                 crypto/schemes.go:206-217
+ *   sign.ThresholdScheme.VerifyRecovered  [kyber v1.1.18 sign/tbls], called at crypto/schemes.go:71,
+ *                                         chain/beacon/chainstore.go:207
+ *   sign.ThresholdScheme.Recover          [kyber v1.1.18 sign/tbls], called at chain/beacon/chainstore.go:202
+ * and adds the batch entry point the serial per-round loops need:
+ *   chain/beacon/sync_manager.go:191-225 (CheckPastBeacons), client/verify.go:139-160, lp2p relays.
+ * INTEGRATION.md shows the cgo binding a drand maintainer would add.
+ */
+#ifndef DRANDHIP_H
+#define DRANDHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* return codes (>= 0 success) */
+#define DH_OK 0
+#define DH_EINVAL (-1)   /* bad argument: unknown scheme, wrong key/sig length, unsupported message shape */
+#define DH_EDEVICE (-2)  /* HIP runtime / kernel failure; the caller should fall back to its CPU path */
+#define DH_ENOMEM (-3)   /* device allocation failed */
+#define DH_EKEY (-4)     /* the group public key does not decode to a subgroup point */
+#define DH_ERECOVER (-5) /* Recover: fewer than t valid partial signatures */
+
+/* scheme ids, in the order of crypto/schemes.go:206-219 plus the RFC 9380 quicknet scheme */
+#define DH_SCHEME_CHAINED 0      /* "pedersen-bls-chained":   sig G2 (96 B), key G1 (48 B), msg SHA256(prev||round) */
+#define DH_SCHEME_UNCHAINED 1    /* "pedersen-bls-unchained": sig G2, key G1, msg SHA256(round) */
+#define DH_SCHEME_G1_LEGACY 2    /* "bls-unchained-on-g1":    sig G1 (48 B), key G2 (96 B), G2 hash DST (legacy) */
+#define DH_SCHEME_G1_RFC9380 3   /* "bls-unchained-g1-rfc9380" (quicknet): sig G1, key G2, G1 hash DST */
+
+/* Select the device (bit i of device_mask = HIP device i; 0 = device 0). Idempotent. */
+int dh_init(uint32_t device_mask);
+/* Release all device resources. Calls after this re-initialise lazily. */
+void dh_shutdown(void);
+
+/* crypto.SchemeFromName: scheme id or DH_EINVAL */
+int dh_scheme_from_name(const char* name);
+/* byte lengths for a scheme: compressed signature / group public key; DH_EINVAL for unknown ids */
+int dh_sig_len(int scheme);
+int dh_key_len(int scheme);
+
+/*
+ * Batch VerifyBeacon over n rounds sharing one group public key.
+ *   pk           compressed key-group point (dh_key_len bytes)
+ *   rounds[i]    round numbers
+ *   sigs         n signatures, record i at sigs + i*sig_stride (sig_stride >= dh_sig_len, multiple of 4)
+ *   prevs        chained scheme only (NULL otherwise): previous signature of round i at prevs + i*prev_stride;
+ *                length prev_lens[i] (or prev_stride when prev_lens is NULL); lengths must be multiples of
+ *                4 and <= 96 (0 = no previous signature, 32 = genesis seed, 96 = stored G2 signature)
+ *   verdict_out  n bytes: 1 = VerifyBeacon returns nil, 0 = it returns an error
+ *   rand_out     n*32 bytes SHA-256(sig) (RandomnessFromSignature) or NULL
+ *   seed         0 = draw the random-linear-combination seed from the OS CSPRNG; otherwise deterministic
+ * Returns DH_OK or a negative error code (no verdicts are valid on error).
+ */
+int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* rounds, const uint8_t* sigs,
+                    size_t sig_stride, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens, size_t n,
+                    uint8_t* verdict_out, uint8_t* rand_out, uint64_t seed);
+
+/*
+ * Same as dh_verify_batch with every array already resident in device memory (HIP device pointers)
+ * and the work enqueued on `hip_stream` (a hipStream_t, NULL = an internal stream). Blocks until done.
+ * `stats_out` (nullable, host) receives {levels, groups_failed, leaf_rounds, rounds_rejected}.
+ */
+int dh_verify_batch_device(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
+                           size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens,
+                           size_t n, uint8_t* d_verdict_out, uint8_t* d_rand_out, uint64_t seed, void* hip_stream,
+                           uint64_t stats_out[4]);
+
+/* Single VerifyBeacon (crypto/schemes.go:70-72): 1 valid, 0 invalid, < 0 error */
+int dh_verify_beacon(int scheme, const uint8_t* pk, size_t pk_len, uint64_t round, const uint8_t* sig, size_t sig_len,
+                     const uint8_t* prev, size_t prev_len);
+
+/* ThresholdScheme.VerifyRecovered(pk, msg, sig) for a 32-byte msg (a beacon digest): 1 / 0 / < 0 */
+int dh_verify_recovered(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* msg32, const uint8_t* sig,
+                        size_t sig_len);
+
+/* crypto.Scheme.DigestBeacon for n rounds (host-side SHA-256, no device): out n*32 bytes */
+int dh_digest_batch(int scheme, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride,
+                    const uint32_t* prev_lens, size_t n, uint8_t* out);
+
+/* RandomnessFromSignature for n signatures on the device: out n*32 bytes */
+int dh_randomness_batch(int scheme, const uint8_t* sigs, size_t sig_stride, size_t n, uint8_t* out);
+
+/*
+ * Batch tbls Recover (kyber sign/tbls Recover + share.RecoverCommit, called at chain/beacon/chainstore.go:202):
+ * for each of n_rounds rounds, partials[part_off[j] .. part_off[j+1]) are (2-byte BE index || sig) records
+ * of (2 + sig_len) bytes for message msgs32[j] (32-byte digests). Each partial is verified against
+ * PubPoly.Eval(index) (commits = t compressed key-group points); the first t valid ones (in the given
+ * order) are kept, sorted by index, and Lagrange-interpolated at 0 in the signature group.
+ * sig_out: n_rounds * sig_len bytes; status_out[j] = 1 recovered, 0 not enough valid partials.
+ */
+int dh_recover_batch(int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
+                     const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* sig_out,
+                     uint8_t* status_out);
+
+/*
+ * Synthetic-chain utilities (test fixtures and benchmark inputs; not part of the verification path):
+ * sign n beacons with a 32-byte big-endian secret scalar, sig_i = [sk] H(DigestBeacon(round_i, prev_i)),
+ * the mock chain pattern of client/test/result/mock/result.go:84-127; and the matching group key [sk] g.
+ * sigs_out: n * dh_sig_len bytes; key_out: dh_key_len bytes.
+ */
+int dh_sign_batch(int scheme, const uint8_t* sk32, const uint64_t* rounds, const uint8_t* prevs, size_t n,
+                  const uint32_t* prev_lens, size_t prev_stride, uint8_t* sigs_out);
+int dh_public_key(int scheme, const uint8_t* sk32, uint8_t* key_out);
+
+/* Human-readable description of the last error on the calling thread ("" if none). */
+const char* dh_last_error_string(void);
+
+/* Build / device description, e.g. "libdrandhip gfx950 ..." */
+const char* dh_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRANDHIP_H */

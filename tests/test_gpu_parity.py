@@ -1,0 +1,142 @@
+"""GPU parity: libdrandhip (gfx950 kernels, through the C ABI) against the CPU oracle, the reference's
+known-answer tests and the committed golden fixtures. Bit-exact verdicts and randomness are required.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from kat import VERIFY_KATS
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+SCHEMES = ["pedersen-bls-chained", "pedersen-bls-unchained", "bls-unchained-on-g1", "bls-unchained-g1-rfc9380"]
+
+
+@pytest.fixture(scope="module")
+def dh():
+    import drand_amd
+    from drand_amd import _lib
+    lib = _lib.load()
+    assert lib.dh_init(0) == 0, _lib.last_error()
+    return drand_amd
+
+
+def _prev_array(prevs):
+    return [bytes.fromhex(p) if isinstance(p, str) else p for p in prevs]
+
+
+@pytest.mark.parametrize("kat", VERIFY_KATS, ids=[k[0] + "-" + str(k[2]) for k in VERIFY_KATS])
+def test_reference_kats(dh, kat):
+    scheme, pk, rnd, sig, prev = kat
+    s = dh.scheme_from_name(scheme)
+    s.verify_beacon(dh.Beacon(rnd, sig, prev), pk)  # raises on failure
+    with pytest.raises(dh.SchemeError):
+        s.verify_beacon(dh.Beacon(rnd + 1, sig, prev), pk)
+    v, rand = s.verify_beacons(pk, [rnd, rnd + 1], np.frombuffer(sig * 2, np.uint8).reshape(2, -1),
+                               [prev, prev] if s.chained else None, seed=7)
+    assert v.tolist() == [True, False]
+    assert rand[0].tobytes() == hashlib.sha256(sig).digest()
+
+
+@pytest.mark.parametrize("scheme", SCHEMES)
+def test_golden_chain(dh, scheme):
+    c = json.load(open(os.path.join(GOLD, "chains.json")))[scheme]
+    s = dh.scheme_from_name(scheme)
+    sigs = np.array([np.frombuffer(bytes.fromhex(x), np.uint8) for x in c["sigs"]])
+    v, rand = s.verify_beacons(bytes.fromhex(c["pk"]), c["rounds"], sigs,
+                               _prev_array(c["prevs"]) if s.chained else None, seed=1)
+    assert v.tolist() == c["valid"]
+    assert [r.tobytes().hex() for r in rand] == c["randomness"]
+
+
+@pytest.mark.parametrize("scheme", SCHEMES)
+def test_golden_negatives(dh, scheme, oracle):
+    c = json.load(open(os.path.join(GOLD, "negatives.json")))[scheme]
+    s = dh.scheme_from_name(scheme)
+    pk = bytes.fromhex(c["pk"])
+    cases = c["cases"]
+    sigs = np.array([np.frombuffer(bytes.fromhex(x["sig"]), np.uint8) for x in cases])
+    rounds = [x["round"] for x in cases]
+    prevs = [bytes.fromhex(x["prev"]) for x in cases] if s.chained else None
+    v, _ = s.verify_beacons(pk, rounds, sigs, prevs, seed=3)
+    assert v.tolist() == [x["valid"] for x in cases], [x["name"] for x in cases]
+    for x in cases:  # single-beacon path
+        b = dh.Beacon(x["round"], bytes.fromhex(x["sig"]), bytes.fromhex(x["prev"]))
+        if x["valid"]:
+            s.verify_beacon(b, pk)
+        else:
+            with pytest.raises(dh.SchemeError):
+                s.verify_beacon(b, pk)
+
+
+def test_chained_replay_faulty_rounds(dh):
+    """CheckPastBeacons semantics (chain/beacon/sync_manager.go:170-235): prev = stored sig of round-1."""
+    rp = json.load(open(os.path.join(GOLD, "replay.json")))
+    s = dh.scheme_from_name("pedersen-bls-chained")
+    stored = [bytes.fromhex(x) for x in rp["stored_sigs"]]
+    prevs = [bytes.fromhex(rp["genesis_seed"])] + stored[:-1]
+    v, _ = s.verify_beacons(bytes.fromhex(rp["pk"]), rp["rounds"], np.array([np.frombuffer(x, np.uint8) for x in stored]),
+                            prevs, seed=11)
+    assert [r for r, ok in zip(rp["rounds"], v) if not ok] == rp["faulty"]
+
+
+@pytest.mark.parametrize("scheme", SCHEMES)
+def test_device_signer_matches_oracle(dh, scheme, oracle):
+    c = json.load(open(os.path.join(GOLD, "chains.json")))[scheme]
+    s = dh.scheme_from_name(scheme)
+    sk = bytes.fromhex(c["sk"])
+    assert s.public_key(sk).hex() == c["pk"]
+    sigs = s.sign_beacons(sk, c["rounds"], _prev_array(c["prevs"]) if s.chained else None)
+    assert [x.tobytes().hex() for x in sigs] == c["sigs"]
+
+
+@pytest.mark.parametrize("scheme", ["bls-unchained-g1-rfc9380", "pedersen-bls-unchained"])
+def test_large_batch_with_corruption(dh, scheme, oracle):
+    """n rounds signed on the device, a seeded set corrupted: exactly those rounds are rejected; the
+    bisection levels (group sizes n, 4096, 64, leaves) run. Corrupted rows are cross-checked on the oracle."""
+    n = 20000 if scheme == "bls-unchained-g1-rfc9380" else 6000
+    s = dh.scheme_from_name(scheme)
+    sk = hashlib.sha256(b"large-" + scheme.encode()).digest()
+    rounds = np.arange(1, n + 1, dtype=np.uint64)
+    sigs = s.sign_beacons(sk, rounds)
+    pk = s.public_key(sk)
+    v, rand = s.verify_beacons(pk, rounds, sigs, seed=5)
+    assert v.all()
+    rng = np.random.default_rng(12345)
+    bad = np.sort(rng.choice(n, size=9, replace=False))
+    sigs2 = sigs.copy()
+    for k, i in enumerate(bad):
+        if k % 3 == 0:
+            sigs2[i] = sigs[(i + 1) % n]              # valid point, wrong signature
+        elif k % 3 == 1:
+            sigs2[i, s.sig_len // 2] ^= 0x04          # bit flip (usually not on the curve)
+        else:
+            sigs2[i, 0] ^= 0x20                       # negated point
+    v2, rand2 = s.verify_beacons(pk, rounds, sigs2, seed=6)
+    assert np.flatnonzero(~v2).tolist() == bad.tolist()
+    for i in bad[:3]:
+        assert not oracle.verify_beacon(scheme, pk, int(rounds[i]), sigs2[i].tobytes())
+    for i in [0, n // 2, n - 1]:
+        assert rand2[i].tobytes() == hashlib.sha256(sigs2[i].tobytes()).digest()
+
+
+def test_seed_independence(dh):
+    c = json.load(open(os.path.join(GOLD, "negatives.json")))["bls-unchained-g1-rfc9380"]
+    s = dh.scheme_from_name("bls-unchained-g1-rfc9380")
+    sigs = np.array([np.frombuffer(bytes.fromhex(x["sig"]), np.uint8) for x in c["cases"]])
+    rounds = [x["round"] for x in c["cases"]]
+    out = [s.verify_beacons(bytes.fromhex(c["pk"]), rounds, sigs, seed=sd)[0].tolist() for sd in (0, 1, 99)]
+    assert out[0] == out[1] == out[2]
+
+
+def test_bad_key_and_arguments(dh):
+    s = dh.scheme_from_name("bls-unchained-g1-rfc9380")
+    with pytest.raises(dh.SchemeError):
+        s.verify_beacons(b"\x00" * 96, [1], np.zeros((1, 48), np.uint8))
+    with pytest.raises(dh.SchemeError):
+        s.verify_beacons(b"\x00" * 95, [1], np.zeros((1, 48), np.uint8))
+    v, _ = s.verify_beacons(VERIFY_KATS[3][1], [], np.zeros((0, 48), np.uint8))
+    assert len(v) == 0
