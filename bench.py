@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""bench.py — verified beacons/sec on MI355X for the quicknet scheme (bls-unchained-g1-rfc9380).
+
+Workload (BASELINE.json configs[1]): batch-verify 1M synthetic quicknet rounds per GPU — G1 signatures,
+G2 group key, RFC 9380 hash-to-G1 — with per-round verdicts and SHA-256 randomness, inputs resident in
+HBM before the timed region. One "step" = one dh_verify_batch_device call over the GPU's 1M rounds (fresh
+CSPRNG seed each step), followed, for N > 1, by an all-gather of the per-GPU verdict bitmaps over RCCL.
+Rounds shard across GPUs (rank r owns rounds r*n+1 .. (r+1)*n): weak scaling, no data-path collective.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rounds n] [--scheme name]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (contract in the task statement): value = rounds verified by all ranks /
+max-over-ranks wall time of the K timed steps. "roofline" reports the dominant kernel's achieved
+integer-multiply rate (algorithmic work of bench/workmodel.json / its HIP-event-measured duration on its
+own stream) against the measured v_mad_u64_u32 peak. "cpu_baseline" times the CPU oracle (a C port of
+the reference's per-round algorithm, oracle/bls_oracle.c) on a bounded sample on the host cores.
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rounds", type=int, default=1 << 20, help="rounds per GPU per step")
+    ap.add_argument("--scheme", default="bls-unchained-g1-rfc9380")
+    ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def load_workmodel():
+    with open(os.path.join(ROOT, "bench", "workmodel.json")) as f:
+        return json.load(f)
+
+
+def cpu_baseline(scheme, pk, rounds, sigs, seconds, threads):
+    """Oracle (port of the reference per-round VerifyBeacon) on `threads` host threads, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ctypes as orc
+    lib = orc.lib()
+    probe = max(threads, 16)
+    t0 = time.perf_counter()
+    v, _ = orc.verify_batch(scheme, pk, rounds[:probe], sigs[:probe], nthreads=threads)
+    dt = time.perf_counter() - t0
+    per = dt / probe
+    n = int(min(len(rounds), max(probe, seconds / max(per, 1e-9))))
+    t0 = time.perf_counter()
+    v, _ = orc.verify_batch(scheme, pk, rounds[:n], sigs[:n], nthreads=threads)
+    dt = time.perf_counter() - t0
+    assert v.all(), "oracle rejected a valid synthetic round"
+    del lib
+    return {"value": n / dt, "unit": "beacons/s", "cores": threads, "kind": "port",
+            "sample": "%d quicknet rounds (first of the 1M synthetic chain), per-round decode+subgroup(r*P)+hash+"
+                      "2-pairing VerifyBeacon, %d threads, %.1f s" % (n, threads, dt)}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    from drand_amd import _lib, scheme_from_name
+
+    lib = _lib.load()
+    rc = lib.dh_init(1 << local)
+    if rc != 0:
+        raise SystemExit("dh_init failed: %s" % _lib.last_error())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    sch = scheme_from_name(args.scheme)
+    n = args.rounds
+    sk = (int.from_bytes(hashlib.sha256(b"drandhip-sk-" + args.scheme.encode()).digest(), "big") %
+          0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001).to_bytes(32, "big")
+    pk = sch.public_key(sk)
+    rounds = np.arange(rank * n + 1, rank * n + n + 1, dtype=np.uint64)
+    t0 = time.perf_counter()
+    sigs = sch.sign_beacons(sk, rounds)  # synthetic chain, signed on the GPU (not timed)
+    t_sign = time.perf_counter() - t0
+
+    d_rounds = torch.from_numpy(rounds.view(np.int64)).to(dev)
+    d_sigs = torch.from_numpy(sigs).to(dev)
+    d_verdict = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_rand = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    stats = (ctypes.c_uint64 * 4)()
+    gathered = [torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev) for _ in range(world)]
+    torch.cuda.synchronize()
+
+    def step(seed=0):
+        rc = lib.dh_verify_batch_device(sch.id, pk, len(pk), ctypes.c_void_p(d_rounds.data_ptr()),
+                                        ctypes.c_void_p(d_sigs.data_ptr()), sch.sig_len, None, 0, None, n,
+                                        ctypes.c_void_p(d_verdict.data_ptr()), ctypes.c_void_p(d_rand.data_ptr()),
+                                        seed, None, stats)
+        if rc != 0:
+            raise RuntimeError("dh_verify_batch_device: %s" % _lib.last_error())
+        if world > 1:
+            dist.all_gather(gathered, _pack(d_verdict))
+
+    for _ in range(args.warmup):
+        step()
+    lib.dh_profile(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    buf = ctypes.create_string_buffer(1 << 16)
+    lib.dh_profile_read(buf, len(buf))
+    lib.dh_profile(0)
+    prof = json.loads(buf.value.decode())
+
+    # sanity (outside the timed region): every synthetic round verifies, randomness = SHA-256(sig)
+    v = d_verdict.cpu().numpy()
+    ok = bool(v.all())
+    r0 = d_rand[0].cpu().numpy().tobytes()
+    ok = ok and r0 == hashlib.sha256(sigs[0].tobytes()).digest()
+
+    if world > 1:
+        t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, bad = float(t[0]), float(t[1])
+        ok = bad == 0.0
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    wm = load_workmodel()
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = world * n * args.steps / elapsed
+    peak = wm["peak_mul32_per_s_measured"]
+    kern = {k: v for k, v in prof.items() if k.startswith("k_prep")}
+    dom = max(kern, key=lambda k: kern[k]["total_ms"]) if kern else None
+    roof = None
+    if dom:
+        avg_s = kern[dom]["total_ms"] / kern[dom]["count"] / 1000.0
+        units = wm["kernel_units_M_per_round"][dom] * wm["mul32_per_M"] * n
+        achieved = units / avg_s / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_r01.json")
+        if os.path.exists(pmc):
+            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+        roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak / 1e12, 3),
+                "unit": "Tmul32/s", "frac": round(achieved * 1e12 / peak, 4), "traffic": traffic,
+                "avg_launch_ms": round(avg_s * 1000, 3)}
+    w_beacon = wm["W_M_per_beacon"]["g2_sig" if sch.sig_len == 96 else "g1_sig"] * wm["mul32_per_M"]
+    out = {
+        "metric": "verified beacons/sec (whole node), quicknet G1 scheme" if sch.id == 3 else
+                  "verified beacons/sec (whole node), %s" % sch.name,
+        "value": round(value, 1), "unit": "beacons/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32 (12x32-bit Montgomery limbs)", "data": "synthetic (GPU-signed chain, seeded key)",
+        "config": {"workload": "%s batch verify, %d rounds per GPU per step" % (sch.name, n), "scheme": sch.name,
+                   "rounds_per_gpu": n, "global_batch": world * n, "parallelism": "round-shard x%d" % world},
+        "roofline": roof,
+        "node_roofline_frac": round(value * w_beacon / (peak * world), 4),
+        "verdicts_ok": ok,
+        "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in prof.items()},
+        "sign_seconds": round(t_sign, 2),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(sch.name, pk, rounds, sigs, args.cpu_sample_seconds, args.cpu_threads)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _pack(d_verdict):
+    """verdict bytes (0/1) -> packed bits, on the device"""
+    import torch
+    n = d_verdict.numel()
+    pad = (-n) % 8
+    v = torch.nn.functional.pad(d_verdict, (0, pad)).view(-1, 8).to(torch.int32)
+    w = torch.tensor([128, 64, 32, 16, 8, 4, 2, 1], dtype=torch.int32, device=d_verdict.device)
+    return (v * w).sum(dim=1).to(torch.uint8)
+
+
+if __name__ == "__main__":
+    main()

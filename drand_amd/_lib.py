@@ -38,6 +38,8 @@ SIGNATURES = {
     "dh_recover_batch": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_int, _c.c_int, _P, _P, _P, _c.c_size_t, _P, _P]),
     "dh_sign_batch": (_c.c_int, [_c.c_int, _c.c_char_p, _P, _P, _c.c_size_t, _P, _c.c_size_t, _P]),
     "dh_public_key": (_c.c_int, [_c.c_int, _c.c_char_p, _P]),
+    "dh_profile": (_c.c_int, [_c.c_int]),
+    "dh_profile_read": (_c.c_int, [_c.c_char_p, _c.c_size_t]),
     "dh_last_error_string": (_c.c_char_p, []),
     "dh_version": (_c.c_char_p, []),
 }

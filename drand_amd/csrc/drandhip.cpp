@@ -261,6 +261,64 @@ dh::msm_geom geom_for(size_t gsize) {
 
 constexpr size_t JAC_WORDS_G1 = 36, JAC_WORDS_G2 = 72;
 
+// ---- live per-kernel timing with HIP events on the launching stream (dh_profile / dh_profile_read)
+struct prof_entry {
+  uint64_t count = 0;
+  double ms = 0;
+};
+struct profiler {
+  std::mutex mu;
+  bool on = false;
+  std::vector<std::pair<std::string, prof_entry>> table;
+  void add(const char* name, float ms) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& e : table)
+      if (e.first == name) {
+        e.second.count++;
+        e.second.ms += ms;
+        return;
+      }
+    prof_entry pe;
+    pe.count = 1;
+    pe.ms = ms;
+    table.emplace_back(name, pe);
+  }
+};
+profiler g_prof;
+
+// records a launch bracketed by events when profiling is on; resolved after the stream syncs
+struct timed_launches {
+  struct rec {
+    const char* name;
+    hipEvent_t a, b;
+  };
+  std::vector<rec> recs;
+  hipStream_t st;
+  explicit timed_launches(hipStream_t s) : st(s) {}
+  template <class F>
+  hipError_t run(const char* name, F&& f) {
+    if (!g_prof.on) return f();
+    rec r{name, nullptr, nullptr};
+    (void)hipEventCreate(&r.a);
+    (void)hipEventCreate(&r.b);
+    (void)hipEventRecord(r.a, st);
+    hipError_t e = f();
+    (void)hipEventRecord(r.b, st);
+    recs.push_back(r);
+    return e;
+  }
+  void resolve() {
+    for (auto& r : recs) {
+      float ms = 0;
+      if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) g_prof.add(r.name, ms);
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+    recs.clear();
+  }
+  ~timed_launches() { resolve(); }
+};
+
 // core pipeline on device-resident inputs
 int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                 size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
@@ -292,9 +350,14 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   HIP_TRY(w->q_pts.ensure(n * jw * 4));
   HIP_TRY(w->scal.ensure(n * 16));
   HIP_TRY(w->entries.ensure(n * 4));
-  HIP_TRY(dh::launch_prep(g2, d_sigs, sig_stride, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), d_rand, st));
-  HIP_TRY(dh::launch_msg(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, n, scheme == DH_SCHEME_CHAINED && d_prevs ? 1 : 0,
-                         dst_id(scheme), w->q_pts.as<uint32_t>(), st));
+  timed_launches T(st);
+  HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>" : "k_prep_sig<fp>", [&] {
+    return dh::launch_prep(g2, d_sigs, sig_stride, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), d_rand, st);
+  }));
+  HIP_TRY(T.run(g2 ? "k_prep_msg<fp2>" : "k_prep_msg<fp>", [&] {
+    return dh::launch_msg(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, n, scheme == DH_SCHEME_CHAINED && d_prevs ? 1 : 0,
+                          dst_id(scheme), w->q_pts.as<uint32_t>(), st);
+  }));
   uint32_t seedw[8];
   int rc = make_seed(seed, seedw);
   if (rc) return rc;
@@ -328,10 +391,14 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(w->pass.ensure(ngroups));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
                   w->buckets.as<uint32_t>(), w->segs.as<uint32_t>()};
-    HIP_TRY(dh::launch_msm(g2, g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(), w->sig_aff.as<uint32_t>(),
-                           w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st));
-    HIP_TRY(dh::launch_group_check(g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups, w->key_aff.as<uint32_t>(),
-                                   w->pass.as<uint8_t>(), st));
+    HIP_TRY(T.run(level == 0 ? "msm_level0" : "msm_bisect", [&] {
+      return dh::launch_msm(g2, g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(), w->sig_aff.as<uint32_t>(),
+                            w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st);
+    }));
+    HIP_TRY(T.run(level == 0 ? "k_group_check_level0" : "k_group_check_bisect", [&] {
+      return dh::launch_group_check(g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups,
+                                    w->key_aff.as<uint32_t>(), w->pass.as<uint8_t>(), st);
+    }));
     HIP_TRY(dh::launch_mark_groups(w->entries.as<uint32_t>(), m, gsize, w->pass.as<uint8_t>(), w->status.as<uint8_t>(),
                                    d_verdict, st));
     w->h_pass.resize(ngroups);
@@ -357,8 +424,10 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(hipMemcpyAsync(w->entries.p, w->h_next.data(), m * 4, hipMemcpyHostToDevice, st));
   }
   if (m > 0) {
-    HIP_TRY(dh::launch_leaf_check(g2, w->entries.as<uint32_t>(), m, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
-                                  w->key_aff.as<uint32_t>(), w->status.as<uint8_t>(), d_verdict, st));
+    HIP_TRY(T.run("k_leaf_check", [&] {
+      return dh::launch_leaf_check(g2, w->entries.as<uint32_t>(), m, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
+                                   w->key_aff.as<uint32_t>(), w->status.as<uint8_t>(), d_verdict, st);
+    }));
     if (stats) stats[2] = m;
   }
   HIP_TRY(hipStreamSynchronize(st));
@@ -602,6 +671,33 @@ int dh_public_key(int scheme, const uint8_t* sk32, uint8_t* key_out) {
   HIP_TRY(hipMemcpyAsync(key_out, w->key_raw.p, kl, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   return DH_OK;
+}
+
+int dh_profile(int enable) {
+  std::lock_guard<std::mutex> lk(g_prof.mu);
+  g_prof.on = enable != 0;
+  g_prof.table.clear();
+  return DH_OK;
+}
+
+int dh_profile_read(char* buf, size_t cap) {
+  std::lock_guard<std::mutex> lk(g_prof.mu);
+  std::string out = "{";
+  bool first = true;
+  for (auto& e : g_prof.table) {
+    char tmp[256];
+    snprintf(tmp, sizeof tmp, "%s\"%s\": {\"count\": %llu, \"total_ms\": %.6f}", first ? "" : ", ", e.first.c_str(),
+             (unsigned long long)e.second.count, e.second.ms);
+    out += tmp;
+    first = false;
+  }
+  out += "}";
+  if (buf && cap) {
+    size_t k = std::min(cap - 1, out.size());
+    memcpy(buf, out.data(), k);
+    buf[k] = 0;
+  }
+  return (int)out.size();
 }
 
 const char* dh_last_error_string(void) { return g_err.c_str(); }

@@ -118,6 +118,14 @@ int dh_sign_batch(int scheme, const uint8_t* sk32, const uint64_t* rounds, const
                   const uint32_t* prev_lens, size_t prev_stride, uint8_t* sigs_out);
 int dh_public_key(int scheme, const uint8_t* sk32, uint8_t* key_out);
 
+/*
+ * Live kernel timing: when enabled, every device stage of the verification path is bracketed by HIP
+ * events on the stream it is launched on; dh_profile_read writes a JSON object
+ * {"stage": {"count": c, "total_ms": t}, ...} into buf (returns the full length). dh_profile resets.
+ */
+int dh_profile(int enable);
+int dh_profile_read(char* buf, size_t cap);
+
 /* Human-readable description of the last error on the calling thread ("" if none). */
 const char* dh_last_error_string(void);
 
