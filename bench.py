@@ -79,6 +79,7 @@ def main():
     import torch
     import torch.distributed as dist
     from drand_amd import _lib, scheme_from_name
+    from drand_amd.dist import gather_verdicts, pack_bits, shard_rounds
 
     lib = _lib.load()
     rc = lib.dh_init(1 << local)
@@ -94,7 +95,7 @@ def main():
     sk = (int.from_bytes(hashlib.sha256(b"drandhip-sk-" + args.scheme.encode()).digest(), "big") %
           0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001).to_bytes(32, "big")
     pk = sch.public_key(sk)
-    rounds = np.arange(rank * n + 1, rank * n + n + 1, dtype=np.uint64)
+    rounds = shard_rounds(rank, world, n)
     t0 = time.perf_counter()
     sigs = sch.sign_beacons(sk, rounds)  # synthetic chain, signed on the GPU (not timed)
     t_sign = time.perf_counter() - t0
@@ -126,7 +127,7 @@ def main():
                 torch.cuda.set_device(local)
                 for k in range(t, k_steps, S):
                     verify(t)
-                    bits[k] = _pack(d_verdict[t])
+                    bits[k] = pack_bits(d_verdict[t])
             except Exception as e:  # surfaced below
                 errs.append(e)
 
@@ -138,9 +139,7 @@ def main():
         if errs:
             raise errs[0]
         if world > 1:  # whole-node verdict bitmaps: one all-gather over RCCL at the end of the batches
-            mine = torch.cat(bits)
-            out = [torch.empty_like(mine) for _ in range(world)]
-            dist.all_gather(out, mine)
+            gather_verdicts(torch.cat(bits), world)
         torch.cuda.synchronize()
 
     run_steps(max(args.warmup, 1) if args.warmup else 0)
@@ -212,16 +211,6 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def _pack(d_verdict):
-    """verdict bytes (0/1) -> packed bits, on the device"""
-    import torch
-    n = d_verdict.numel()
-    pad = (-n) % 8
-    v = torch.nn.functional.pad(d_verdict, (0, pad)).view(-1, 8).to(torch.int32)
-    w = torch.tensor([128, 64, 32, 16, 8, 4, 2, 1], dtype=torch.int32, device=d_verdict.device)
-    return (v * w).sum(dim=1).to(torch.uint8)
 
 
 if __name__ == "__main__":

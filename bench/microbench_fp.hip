@@ -11,13 +11,19 @@ constexpr int IT = 256;
 __global__ void k_cios(dh::fp* out, const dh::fp* in) {
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   dh::fp x = in[gid & 1023], y = in[(gid + 1) & 1023], z = in[(gid + 2) & 1023];
-  for (int it = 0; it < IT; it++) { x = dh::fp_mul(x, y); z = dh::fp_mul(z, y); }
+  for (int it = 0; it < IT; it++) { x = dh::fp_mul_cios(x, y); z = dh::fp_mul_cios(z, y); }
   out[gid] = dh::fp_add(x, z);
 }
 __global__ void k_fips(dh::fp* out, const dh::fp* in) {
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   dh::fp x = in[gid & 1023], y = in[(gid + 1) & 1023], z = in[(gid + 2) & 1023];
   for (int it = 0; it < IT; it++) { dh::fips_mont_mul(x.v, x.v, y.v); dh::fips_mont_mul(z.v, z.v, y.v); }
+  out[gid] = dh::fp_add(x, z);
+}
+__global__ void k_fipsc(dh::fp* out, const dh::fp* in) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  dh::fp x = in[gid & 1023], y = in[(gid + 1) & 1023], z = in[(gid + 2) & 1023];
+  for (int it = 0; it < IT; it++) { dh::fips_mont_mul_c(x.v, x.v, y.v); dh::fips_mont_mul_c(z.v, z.v, y.v); }
   out[gid] = dh::fp_add(x, z);
 }
 __global__ void k_fsqr(dh::fp* out, const dh::fp* in) {
@@ -29,7 +35,7 @@ __global__ void k_fsqr(dh::fp* out, const dh::fp* in) {
 __global__ void k_csqr(dh::fp* out, const dh::fp* in) {
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   dh::fp x = in[gid & 1023], z = in[(gid + 2) & 1023];
-  for (int it = 0; it < IT; it++) { x = dh::fp_mul(x, x); z = dh::fp_mul(z, z); }
+  for (int it = 0; it < IT; it++) { x = dh::fp_mul_cios(x, x); z = dh::fp_mul_cios(z, z); }
   out[gid] = dh::fp_add(x, z);
 }
 
@@ -85,6 +91,9 @@ int main() {
     hipLaunchKernelGGL(k_fips, dim3(4), dim3(256), 0, 0, o1, in);
     hipLaunchKernelGGL(k_cios, dim3(4), dim3(256), 0, 0, o2, in);
     hipLaunchKernelGGL(k_fsqr, dim3(4), dim3(256), 0, 0, o1 + 1024, in);
+    static dh::fp r3[1024];
+    hipLaunchKernelGGL(k_fipsc, dim3(4), dim3(256), 0, 0, o2 + 2048, in);
+    hipMemcpy(r3, o2 + 2048, sizeof(r3), hipMemcpyDeviceToHost);
     hipLaunchKernelGGL(k_csqr, dim3(4), dim3(256), 0, 0, o2 + 1024, in);
     static dh::fp r1[2048], r2[2048];
     hipMemcpy(r1, o1, sizeof(r1), hipMemcpyDeviceToHost);
@@ -101,6 +110,7 @@ int main() {
       if (ge) { u128 br = 0; for (int i = 0; i < 6; i++) { u128 d = (u128)t[i] - P64[i] - br; t[i] = (uint64_t)d; br = (d >> 64) & 1; } }
       if (memcmp(t, r1[g].v, 48)) bad |= 1;
       if (memcmp(t, r2[g].v, 48)) bad |= 2;
+      if (memcmp(t, r3[g].v, 48)) bad |= 8;
     }
     for (int g = 0; g < 1024; g++) if (memcmp(r1[1024 + g].v, r2[1024 + g].v, 48)) bad |= 4;
   }
@@ -110,6 +120,8 @@ int main() {
   printf("{\"op\": \"fp_mul_cios\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
   ms = tk(k_fips, blocks, o1, in);
   printf("{\"op\": \"fp_mul_fips\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
+  ms = tk(k_fipsc, blocks, o1, in);
+  printf("{\"op\": \"fp_mul_fips_plain_c\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
   ms = tk(k_csqr, blocks, o1, in);
   printf("{\"op\": \"fp_sqr_cios\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
   ms = tk(k_fsqr, blocks, o1, in);

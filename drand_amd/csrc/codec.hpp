@@ -11,7 +11,7 @@
 // Subgroup tests (exact for BLS12-381): G1  phi(P) == [-u^2] P  with phi(x, y) = (beta x, y);
 //                                      G2  psi(P) == [u] P.
 #pragma once
-#include "curve.hpp"
+#include "h2c.hpp"
 
 namespace dh {
 
@@ -40,14 +40,6 @@ DH_DEV bool g1_in_subgroup(const aff<fp>& p) {
   t = jac_mul_uabs_j(t);
   jac<fp> phi = jac_from_aff(aff<fp>{fp_mul(p.x, fp_c(cst::BETA)), p.y});
   return jac_eq(phi, jac_neg(t));
-}
-
-DH_DEV jac<fp2> g2_psi(const jac<fp2>& p) {
-  jac<fp2> r;
-  r.x = fp2_mul(fp2_conj(p.x), fp2_c(cst::PSI_X));
-  r.y = fp2_mul(fp2_conj(p.y), fp2_c(cst::PSI_Y));
-  r.z = fp2_conj(p.z);
-  return r;
 }
 
 DH_DEV bool g2_in_subgroup(const aff<fp2>& p) {

@@ -18,6 +18,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -86,6 +87,10 @@ struct worker {
   dbuf key_raw, key_aff, key_ok;
   // MSM
   dbuf cnt, off, scan_tmp, list, buckets, segs, outA, outB, pass;
+  // tbls Recover
+  dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
+      r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
+      r_sigbytes, r_status2, r_aff2, r_entries2;
   std::vector<uint8_t> h_pass;
   // decoded group key cache: the same key is used for every batch of a chain
   uint8_t cached_key[96];
@@ -96,7 +101,10 @@ struct worker {
   void release_all() {
     dbuf* all[] = {&status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
-                   &scan_tmp, &list, &buckets, &segs, &outA, &outB, &pass};
+                   &scan_tmp, &list, &buckets, &segs, &outA, &outB, &pass, &r_commits, &r_cstatus, &r_caff, &r_shares,
+                   &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
+                   &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
@@ -453,6 +461,403 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   return DH_OK;
 }
 
+// ---- scalar field F_r on the host (Lagrange coefficients; 4 x 64-bit Montgomery, R = 2^256)
+struct fr {
+  uint64_t v[4];
+};
+const uint64_t FR_R[4] = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL, 0x73eda753299d7d48ULL};
+const uint64_t FR_N0 = 0xfffffffeffffffffULL;  // -r^-1 mod 2^64
+typedef unsigned __int128 u128;
+
+bool fr_geq(const uint64_t* a, const uint64_t* b) {
+  for (int i = 3; i >= 0; i--) {
+    if (a[i] != b[i]) return a[i] > b[i];
+  }
+  return true;
+}
+void fr_subr(uint64_t* a) {
+  u128 br = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 d = (u128)a[i] - FR_R[i] - br;
+    a[i] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+}
+fr fr_mul(const fr& a, const fr& b) {
+  uint64_t t[6] = {0};
+  for (int i = 0; i < 4; i++) {
+    u128 c = 0;
+    for (int j = 0; j < 4; j++) {
+      c += (u128)a.v[j] * b.v[i] + t[j];
+      t[j] = (uint64_t)c;
+      c >>= 64;
+    }
+    u128 s2 = (u128)t[4] + c;
+    t[4] = (uint64_t)s2;
+    t[5] = (uint64_t)(s2 >> 64);
+    uint64_t m = t[0] * FR_N0;
+    c = (u128)m * FR_R[0] + t[0];
+    c >>= 64;
+    for (int j = 1; j < 4; j++) {
+      c += (u128)m * FR_R[j] + t[j];
+      t[j - 1] = (uint64_t)c;
+      c >>= 64;
+    }
+    s2 = (u128)t[4] + c;
+    t[3] = (uint64_t)s2;
+    t[4] = t[5] + (uint64_t)(s2 >> 64);
+  }
+  fr r;
+  memcpy(r.v, t, 32);
+  if (t[4] || fr_geq(r.v, FR_R)) fr_subr(r.v);
+  return r;
+}
+fr fr_from_u64(uint64_t x) {  // Montgomery form of a small integer
+  static fr r2;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    uint64_t t[4] = {1, 0, 0, 0};
+    for (int i = 0; i < 512; i++) {  // 2^512 mod r by doubling
+      uint64_t c = 0;
+      for (int k = 0; k < 4; k++) {
+        uint64_t nv = (t[k] << 1) | c;
+        c = t[k] >> 63;
+        t[k] = nv;
+      }
+      if (c || fr_geq(t, FR_R)) fr_subr(t);
+    }
+    memcpy(r2.v, t, 32);
+  });
+  fr a = {{x, 0, 0, 0}};
+  return fr_mul(a, r2);
+}
+fr fr_sub(const fr& a, const fr& b) {
+  fr r;
+  u128 br = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 d = (u128)a.v[i] - b.v[i] - br;
+    r.v[i] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  if (br) {
+    u128 c = 0;
+    for (int i = 0; i < 4; i++) {
+      c += (u128)r.v[i] + FR_R[i];
+      r.v[i] = (uint64_t)c;
+      c >>= 64;
+    }
+  }
+  return r;
+}
+fr fr_inv(const fr& a) {  // a^(r-2)
+  uint64_t e[4];
+  memcpy(e, FR_R, 32);
+  e[0] -= 2;
+  fr acc = fr_from_u64(1);
+  for (int i = 255; i >= 0; i--) {
+    acc = fr_mul(acc, acc);
+    if ((e[i >> 6] >> (i & 63)) & 1) acc = fr_mul(acc, a);
+  }
+  return acc;
+}
+void fr_to_words(const fr& a, uint32_t out[8]) {  // leave Montgomery form, little-endian 32-bit words
+  fr one = {{1, 0, 0, 0}};
+  fr p = fr_mul(a, one);
+  for (int i = 0; i < 4; i++) {
+    out[2 * i] = (uint32_t)p.v[i];
+    out[2 * i + 1] = (uint32_t)(p.v[i] >> 32);
+  }
+}
+// Lagrange basis at 0 over x_k = idx_k + 1 (share.RecoverCommit / lagrangeBasis [kyber v1.1.18 share/poly.go])
+void lagrange_at_zero(const std::vector<uint32_t>& idx, uint32_t* out /* t x 8 words */) {
+  const size_t t = idx.size();
+  std::vector<fr> den(t), num(t);
+  for (size_t k = 0; k < t; k++) {
+    fr xk = fr_from_u64((uint64_t)idx[k] + 1);
+    fr n = fr_from_u64(1), d = fr_from_u64(1);
+    for (size_t m = 0; m < t; m++) {
+      if (m == k) continue;
+      fr xm = fr_from_u64((uint64_t)idx[m] + 1);
+      n = fr_mul(n, xm);
+      d = fr_mul(d, fr_sub(xm, xk));
+    }
+    num[k] = n;
+    den[k] = d;
+  }
+  // batch inversion of the denominators
+  std::vector<fr> pre(t);
+  fr acc = fr_from_u64(1);
+  for (size_t k = 0; k < t; k++) {
+    pre[k] = acc;
+    acc = fr_mul(acc, den[k]);
+  }
+  fr inv = fr_inv(acc);
+  for (size_t k = t; k-- > 0;) {
+    fr dk_inv = fr_mul(inv, pre[k]);
+    inv = fr_mul(inv, den[k]);
+    fr_to_words(fr_mul(num[k], dk_inv), out + 8 * k);
+  }
+}
+
+int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
+                 const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* sig_out, uint8_t* status_out,
+                 hipStream_t st) {
+  const bool g2 = sig_on_g2(scheme);
+  const int sl = g2 ? 96 : 48, kl = g2 ? 48 : 96;
+  const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1, aw = jw * 2 / 3;
+  const size_t kjw = g2 ? JAC_WORDS_G1 : JAC_WORDS_G2, kaw = kjw * 2 / 3;
+  const size_t np = part_off[n_rounds] - part_off[0];
+  const uint32_t base = part_off[0];
+  memset(status_out, 0, n_rounds);
+  if (n_rounds == 0) return DH_OK;
+  timed_launches T(st);
+  // 1. commits -> affine key-group points, all must decode
+  HIP_TRY(w->r_commits.ensure((size_t)t * kl));
+  HIP_TRY(w->r_cstatus.ensure(t));
+  HIP_TRY(w->r_caff.ensure((size_t)t * kaw * 4));
+  HIP_TRY(hipMemcpyAsync(w->r_commits.p, commits, (size_t)t * kl, hipMemcpyHostToDevice, st));
+  HIP_TRY(dh::launch_prep(g2 ? 0 : 1, w->r_commits.as<uint8_t>(), kl, t, w->r_cstatus.as<uint8_t>(),
+                          w->r_caff.as<uint32_t>(), nullptr, st));
+  std::vector<uint8_t> cst(t);
+  HIP_TRY(hipMemcpyAsync(cst.data(), w->r_cstatus.p, t, hipMemcpyDeviceToHost, st));
+  // 2. public shares
+  HIP_TRY(w->r_shares.ensure((size_t)n_nodes * kjw * 4));
+  HIP_TRY(T.run("k_pubpoly_eval", [&] {
+    return dh::launch_pubpoly_eval(g2 ? 0 : 1, w->r_caff.as<uint32_t>(), t, n_nodes, w->r_shares.as<uint32_t>(), st);
+  }));
+  // 3./4. partials: repack, decode + subgroup check
+  HIP_TRY(w->r_raw.ensure(np * (2 + sl) + 4));
+  HIP_TRY(w->r_psigs.ensure(np * sl + 4));
+  HIP_TRY(w->r_pidx.ensure(np * 4 + 4));
+  HIP_TRY(w->r_pstatus.ensure(np + 4));
+  HIP_TRY(w->r_paff.ensure(np * aw * 4 + 16));
+  HIP_TRY(hipMemcpyAsync(w->r_raw.p, partials + (size_t)base * (2 + sl), np * (2 + sl), hipMemcpyHostToDevice, st));
+  HIP_TRY(dh::launch_repack_partials(w->r_raw.as<uint8_t>(), np, sl, w->r_psigs.as<uint8_t>(), w->r_pidx.as<uint32_t>(), st));
+  HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>(partials)" : "k_prep_sig<fp>(partials)", [&] {
+    return dh::launch_prep(g2, w->r_psigs.as<uint8_t>(), sl, np, w->r_pstatus.as<uint8_t>(), w->r_paff.as<uint32_t>(),
+                           nullptr, st);
+  }));
+  // 5. hash points of the round messages
+  HIP_TRY(w->r_msgs.ensure(n_rounds * 32));
+  HIP_TRY(w->r_q.ensure(n_rounds * jw * 4));
+  HIP_TRY(hipMemcpyAsync(w->r_msgs.p, msgs32, n_rounds * 32, hipMemcpyHostToDevice, st));
+  HIP_TRY(T.run(g2 ? "k_prep_msg32<fp2>" : "k_prep_msg32<fp>", [&] {
+    return dh::launch_msg32(g2, w->r_msgs.as<uint8_t>(), n_rounds, dst_id(scheme), w->r_q.as<uint32_t>(), st);
+  }));
+  // 6. per-partial round, share index (host parse), signer-sorted entry lists
+  std::vector<uint32_t> round_of(np), share(np);
+  for (size_t j = 0; j < n_rounds; j++)
+    for (uint32_t e = part_off[j]; e < part_off[j + 1]; e++) round_of[e - base] = (uint32_t)j;
+  for (size_t e = 0; e < np; e++) {
+    const uint8_t* r = partials + (size_t)(base + e) * (2 + sl);
+    share[e] = ((uint32_t)r[0] << 8) | r[1];
+  }
+  std::vector<uint32_t> cnt(n_nodes + 1, 0);
+  for (size_t e = 0; e < np; e++)
+    if (share[e] < (uint32_t)n_nodes) cnt[share[e] + 1]++;
+  for (int i = 0; i < n_nodes; i++) cnt[i + 1] += cnt[i];
+  const size_t mB = cnt[n_nodes];
+  std::vector<uint32_t> e_pidx(mB), e_sidx(mB), e_grp(mB), cur(cnt.begin(), cnt.end() - 1);
+  for (size_t e = 0; e < np; e++) {
+    if (share[e] >= (uint32_t)n_nodes) continue;
+    uint32_t pos = cur[share[e]]++;
+    e_pidx[pos] = round_of[e];
+    e_sidx[pos] = (uint32_t)e;
+    e_grp[pos] = share[e];
+  }
+  HIP_TRY(w->r_round_of.ensure(np * 4 + 4));
+  HIP_TRY(w->r_e_pidx.ensure(mB * 4 + 4));
+  HIP_TRY(w->r_e_sidx.ensure(mB * 4 + 4));
+  HIP_TRY(w->r_e_grp.ensure(mB * 4 + 4));
+  HIP_TRY(hipMemcpyAsync(w->r_round_of.p, round_of.data(), np * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->r_e_pidx.p, e_pidx.data(), mB * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->r_e_sidx.p, e_sidx.data(), mB * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->r_e_grp.p, e_grp.data(), mB * 4, hipMemcpyHostToDevice, st));
+  // 7. RLC scalars per partial
+  uint32_t seedw[8];
+  int rc = make_seed(0, seedw);
+  if (rc) return rc;
+  HIP_TRY(w->key_ok.ensure(64));
+  uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
+  HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
+  HIP_TRY(w->r_scal.ensure(np * 16 + 16));
+  HIP_TRY(dh::launch_scalars(d_seed, np, w->r_pstatus.as<uint8_t>(), w->r_scal.as<uint4>(), st));
+  HIP_TRY(hipStreamSynchronize(st));
+  for (int c = 0; c < t; c++)
+    if (cst[c] != 1) return fail(DH_EKEY, "public polynomial commitment %d does not decode to a subgroup point", c);
+  // 8./9. MSMs: A = sum r sigma (one group), B_i = sum r Q_round per signer i
+  HIP_TRY(w->r_ok.ensure(np + 4));
+  bool batch_ok = false;
+  {
+    HIP_TRY(w->entries.ensure(np * 4 + 4));
+    HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), np, st));
+    const dh::msm_geom gA = geom_for(std::max<size_t>(np, 1));
+    size_t avg = std::max<size_t>(1, mB / std::max(1, n_nodes));
+    dh::msm_geom gB = geom_for(avg);
+    while (gB.c > 3 && (size_t)n_nodes * gB.nwin * gB.nbuck > ((size_t)1 << 24)) gB = geom_for(((size_t)1 << (gB.c + 1)));
+    const size_t nkA = (size_t)gA.nwin * gA.nbuck, nkB = (size_t)n_nodes * gB.nwin * gB.nbuck;
+    const size_t nk = std::max(nkA, nkB);
+    HIP_TRY(w->cnt.ensure(nk * 4));
+    HIP_TRY(w->off.ensure((nk + 1) * 4));
+    HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
+    HIP_TRY(w->list.ensure(std::max(np * gA.nwin, mB * gB.nwin) * 4 + 4));
+    HIP_TRY(w->buckets.ensure(nk * jw * 4));
+    HIP_TRY(w->segs.ensure(std::max((size_t)gA.nwin * gA.nseg, (size_t)n_nodes * gB.nwin * gB.nseg) * jw * 4));
+    HIP_TRY(w->outA.ensure(jw * 4));
+    HIP_TRY(w->outB.ensure((size_t)n_nodes * jw * 4));
+    dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
+                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>()};
+    HIP_TRY(T.run("recover_msm_sigs", [&] {
+      hipError_t e = dh::launch_msm_sort(gA, w->entries.as<uint32_t>(), nullptr, nullptr, np, 1, w->r_scal.as<uint4>(), ws, st);
+      if (e != hipSuccess) return e;
+      return dh::launch_msm_points(g2, 1, gA, 1, w->r_paff.as<uint32_t>(), ws, w->outA.as<uint32_t>(), st);
+    }));
+    HIP_TRY(T.run("recover_msm_hash_by_signer", [&] {
+      hipError_t e = dh::launch_msm_sort(gB, w->r_e_pidx.as<uint32_t>(), w->r_e_sidx.as<uint32_t>(), w->r_e_grp.as<uint32_t>(),
+                                         mB, n_nodes, w->r_scal.as<uint4>(), ws, st);
+      if (e != hipSuccess) return e;
+      return dh::launch_msm_points(g2, 0, gB, n_nodes, w->r_q.as<uint32_t>(), ws, w->outB.as<uint32_t>(), st);
+    }));
+    // 10. multi-pairing: n_nodes + 1 pairs
+    const size_t npairs = (size_t)n_nodes + 1;
+    HIP_TRY(w->r_P.ensure(npairs * JAC_WORDS_G1 * 4));
+    HIP_TRY(w->r_Q.ensure(npairs * JAC_WORDS_G2 * 4));
+    HIP_TRY(w->r_f.ensure(npairs * 144 * 4));
+    HIP_TRY(w->r_skip.ensure(npairs + 4));
+    HIP_TRY(w->pass.ensure(16));
+    HIP_TRY(T.run("recover_pair_check", [&] {
+      hipError_t e = dh::launch_recover_pairs(g2, w->r_shares.as<uint32_t>(), w->outB.as<uint32_t>(), w->outA.as<uint32_t>(),
+                                              n_nodes, w->r_P.as<uint32_t>(), w->r_Q.as<uint32_t>(), st);
+      if (e != hipSuccess) return e;
+      return dh::launch_pair_check(w->r_P.as<uint32_t>(), w->r_Q.as<uint32_t>(), npairs, 0, 0, nullptr, w->r_f.as<uint32_t>(),
+                                   w->r_skip.as<uint8_t>(), w->pass.as<uint8_t>(), st);
+    }));
+    uint8_t pass = 0;
+    HIP_TRY(hipMemcpyAsync(&pass, w->pass.p, 1, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    batch_ok = pass == 1;
+  }
+  // 11. per-partial validity
+  std::vector<uint8_t> ok(np);
+  if (batch_ok) {
+    HIP_TRY(hipMemcpyAsync(ok.data(), w->r_pstatus.p, np, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (size_t e = 0; e < np; e++) ok[e] = (ok[e] == 1 && share[e] < (uint32_t)n_nodes) ? 1 : 0;
+  } else {
+    HIP_TRY(T.run("k_partial_leaf", [&] {
+      return dh::launch_partial_leaf(g2, w->entries.as<uint32_t>(), np, w->r_paff.as<uint32_t>(), w->r_pstatus.as<uint8_t>(),
+                                     w->r_pidx.as<uint32_t>(), w->r_round_of.as<uint32_t>(), w->r_q.as<uint32_t>(),
+                                     w->r_shares.as<uint32_t>(), n_nodes, w->r_ok.as<uint8_t>(), st);
+    }));
+    HIP_TRY(hipMemcpyAsync(ok.data(), w->r_ok.p, np, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  // 12. selection (first t valid in the given order; sorted by index; duplicates dropped) + Lagrange sets
+  std::vector<uint32_t> sel(n_rounds * (size_t)t, 0), lamset(n_rounds, 0);
+  std::vector<uint8_t> rok(n_rounds, 0);
+  std::vector<std::vector<uint32_t>> sets;
+  std::vector<uint32_t> lam;
+  std::map<std::vector<uint32_t>, uint32_t> set_id;
+  for (size_t j = 0; j < n_rounds; j++) {
+    std::vector<std::pair<uint32_t, uint32_t>> kept;  // (share index, partial id)
+    for (uint32_t e = part_off[j] - base; e < part_off[j + 1] - base && kept.size() < (size_t)t; e++)
+      if (ok[e]) kept.emplace_back(share[e], e);
+    if (kept.size() < (size_t)t) continue;
+    std::stable_sort(kept.begin(), kept.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    std::vector<uint32_t> idx;
+    std::vector<uint32_t> pid;
+    for (auto& k : kept) {
+      if (!idx.empty() && idx.back() == k.first) continue;
+      idx.push_back(k.first);
+      pid.push_back(k.second);
+    }
+    if (idx.size() < (size_t)t) continue;
+    auto it = set_id.find(idx);
+    uint32_t sid;
+    if (it == set_id.end()) {
+      sid = (uint32_t)sets.size();
+      set_id.emplace(idx, sid);
+      sets.push_back(idx);
+      lam.resize(lam.size() + (size_t)t * 8);
+      lagrange_at_zero(idx, lam.data() + (size_t)sid * t * 8);
+    } else {
+      sid = it->second;
+    }
+    for (int k = 0; k < t; k++) sel[j * t + k] = pid[k];
+    lamset[j] = sid;
+    rok[j] = 1;
+  }
+  if (sets.empty()) lam.assign((size_t)t * 8, 0);
+  // 13. interpolation on the device
+  HIP_TRY(w->r_sel.ensure(sel.size() * 4));
+  HIP_TRY(w->r_lam.ensure(lam.size() * 4));
+  HIP_TRY(w->r_lamset.ensure(n_rounds * 4));
+  HIP_TRY(w->r_rok.ensure(n_rounds));
+  HIP_TRY(w->r_sig.ensure(n_rounds * jw * 4));
+  HIP_TRY(hipMemcpyAsync(w->r_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->r_lam.p, lam.data(), lam.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->r_lamset.p, lamset.data(), n_rounds * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->r_rok.p, rok.data(), n_rounds, hipMemcpyHostToDevice, st));
+  HIP_TRY(T.run("k_lagrange", [&] {
+    return dh::launch_lagrange(g2, w->r_sel.as<uint32_t>(), w->r_lam.as<uint32_t>(), w->r_lamset.as<uint32_t>(),
+                               w->r_rok.as<uint8_t>(), t, n_rounds, w->r_paff.as<uint32_t>(), w->r_sig.as<uint32_t>(), st);
+  }));
+  // 14./15. compress, then VerifyRecovered (chainstore.go:207) as one batch against the group key (commit 0)
+  HIP_TRY(w->r_sigbytes.ensure(n_rounds * sl));
+  HIP_TRY(dh::launch_compress(g2, w->r_sig.as<uint32_t>(), n_rounds, w->r_sigbytes.as<uint8_t>(), st));
+  HIP_TRY(hipMemcpyAsync(sig_out, w->r_sigbytes.p, n_rounds * sl, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  // verify through the regular batch path (messages are given digests: use the per-round hash points)
+  std::vector<uint8_t> vv(n_rounds, 0);
+  {
+    HIP_TRY(w->r_status2.ensure(n_rounds));
+    HIP_TRY(w->r_aff2.ensure(n_rounds * aw * 4));
+    HIP_TRY(w->r_entries2.ensure(n_rounds * 4));
+    HIP_TRY(dh::launch_prep(g2, w->r_sigbytes.as<uint8_t>(), sl, n_rounds, w->r_status2.as<uint8_t>(),
+                            w->r_aff2.as<uint32_t>(), nullptr, st));
+    HIP_TRY(dh::launch_scalars(d_seed, n_rounds, w->r_status2.as<uint8_t>(), w->r_scal.as<uint4>(), st));
+    HIP_TRY(dh::launch_iota(w->r_entries2.as<uint32_t>(), n_rounds, st));
+    // group key = commit 0 (affine, key group) — staged where the group check expects it
+    HIP_TRY(hipMemcpyAsync(w->key_aff.p, w->r_caff.p, kaw * 4, hipMemcpyDeviceToDevice, st));
+    w->cached_key_len = 0;  // key_aff now holds this call's key
+    const dh::msm_geom g = geom_for(n_rounds);
+    const size_t nk = (size_t)g.nwin * g.nbuck;
+    HIP_TRY(w->cnt.ensure(nk * 4));
+    HIP_TRY(w->off.ensure((nk + 1) * 4));
+    HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
+    HIP_TRY(w->list.ensure(n_rounds * g.nwin * 4));
+    HIP_TRY(w->buckets.ensure(nk * jw * 4));
+    HIP_TRY(w->segs.ensure((size_t)g.nwin * g.nseg * jw * 4));
+    dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
+                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>()};
+    HIP_TRY(T.run("recover_verify", [&] {
+      hipError_t e = dh::launch_msm(g2, g, w->r_entries2.as<uint32_t>(), n_rounds, 1, w->r_scal.as<uint4>(),
+                                    w->r_aff2.as<uint32_t>(), w->r_q.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
+                                    w->outB.as<uint32_t>(), st);
+      if (e != hipSuccess) return e;
+      return dh::launch_group_check(g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), 1, w->key_aff.as<uint32_t>(),
+                                    w->pass.as<uint8_t>(), st);
+    }));
+    uint8_t pass = 0, dummy = 0;
+    (void)dummy;
+    HIP_TRY(hipMemcpyAsync(&pass, w->pass.p, 1, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(w->r_ok.ensure(std::max(np, n_rounds) + 4));
+    if (pass == 1) {
+      HIP_TRY(hipMemcpyAsync(vv.data(), w->r_status2.p, n_rounds, hipMemcpyDeviceToHost, st));
+    } else {
+      HIP_TRY(hipMemsetAsync(w->r_ok.p, 0, n_rounds, st));
+      HIP_TRY(dh::launch_leaf_check(g2, w->r_entries2.as<uint32_t>(), n_rounds, w->r_aff2.as<uint32_t>(),
+                                    w->r_q.as<uint32_t>(), w->key_aff.as<uint32_t>(), w->r_status2.as<uint8_t>(),
+                                    w->r_ok.as<uint8_t>(), st));
+      HIP_TRY(hipMemcpyAsync(vv.data(), w->r_ok.p, n_rounds, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  for (size_t j = 0; j < n_rounds; j++) status_out[j] = (rok[j] && vv[j] == 1) ? 1 : 0;
+  return DH_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -616,9 +1021,18 @@ int dh_randomness_batch(int scheme, const uint8_t* sigs, size_t sig_stride, size
 int dh_recover_batch(int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
                      const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* sig_out,
                      uint8_t* status_out) {
-  (void)scheme; (void)commits; (void)t; (void)n_nodes; (void)msgs32; (void)partials; (void)part_off; (void)n_rounds;
-  (void)sig_out; (void)status_out;
-  return fail(DH_EINVAL, "dh_recover_batch: not yet implemented on the device path");
+  if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
+  if (t < 1 || n_nodes < 1 || n_nodes > 65535 || !commits || (n_rounds && (!msgs32 || !partials || !part_off ||
+                                                                          !sig_out || !status_out)))
+    return fail(DH_EINVAL, "bad Recover arguments");
+  for (size_t j = 0; j < n_rounds; j++)
+    if (part_off[j + 1] < part_off[j]) return fail(DH_EINVAL, "part_off must be non-decreasing");
+  lease L;
+  if (L.rc) return L.rc;
+  int rc = set_device_and_stream(L.w);
+  if (rc) return rc;
+  return recover_core(L.w, scheme, commits, t, n_nodes, msgs32, partials, part_off, n_rounds, sig_out, status_out,
+                      L.w->stream);
 }
 
 static void sk_words(const uint8_t* sk32, uint32_t w[8]) {

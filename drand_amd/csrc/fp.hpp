@@ -16,6 +16,9 @@
 namespace dh {
 
 #define DH_DEV __device__ __forceinline__
+// out-of-line helper (a real call); the field products themselves are the out-of-line fp_mul_vec /
+// fp_sqr_vec (measured: point formulas must stay inline — by-reference arguments go through scratch)
+#define DH_OOL __device__ __noinline__
 
 struct fp {
   uint32_t v[12];
@@ -278,11 +281,32 @@ DH_DEV fp fp_pow_words(const fp& x, const uint32_t* e, int nbits) {
   return acc;
 }
 
-DH_DEV fp fp_inv(const fp& x) { return fp_pow_words(x, cst::EXP_P_MINUS_2, cst::EXP_P_MINUS_2_BITS); }
+// x^e for a fixed exponent given as a sliding-window schedule (consts.hpp SCHED_*, w = 3):
+// table x, x^3, x^5, x^7; sched[0] = first table index, then (squarings << 8 | index), index 0xff =
+// squarings only. 378 squarings + ~105 multiplications for the 381-bit exponents (binary: ~228).
+DH_DEV fp fp_pow_sched(const fp& x, const uint16_t* sched, int len) {
+  const fp x2 = fp_sqr(x);
+  const fp t1 = fp_mul(x, x2);
+  const fp t2 = fp_mul(t1, x2);
+  const fp t3 = fp_mul(t2, x2);
+  auto pick = [&](uint32_t k) { return k == 0 ? x : (k == 1 ? t1 : (k == 2 ? t2 : t3)); };
+  fp acc = pick(sched[0]);
+#pragma unroll 1
+  for (int i = 1; i < len; i++) {
+    const uint32_t op = sched[i];
+    const uint32_t nsq = op >> 8, k = op & 0xff;
+#pragma unroll 1
+    for (uint32_t j = 0; j < nsq; j++) acc = fp_sqr(acc);
+    if (k != 0xff) acc = fp_mul(acc, pick(k));
+  }
+  return acc;
+}
+
+DH_DEV fp fp_inv(const fp& x) { return fp_pow_sched(x, cst::SCHED_INV, cst::SCHED_INV_LEN); }
 
 // returns true and r = sqrt(a) if a is a square
 DH_DEV bool fp_sqrt(fp& r, const fp& a) {
-  r = fp_pow_words(a, cst::EXP_P_PLUS_1_DIV_4, cst::EXP_P_PLUS_1_DIV_4_BITS);
+  r = fp_pow_sched(a, cst::SCHED_SQRT, cst::SCHED_SQRT_LEN);
   return fp_eq(fp_sqr(r), a);
 }
 

@@ -12,12 +12,17 @@
 
 namespace dh {
 
-// acc(64) += x*y, carry into hi32
-#define DH_MAC(acc, hi, x, y)                                                          \
-  asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" \
-               : "+v"(acc), "+v"(hi)                                                   \
-               : "v"(x), "v"(y)                                                        \
-               : "vcc")
+// acc(64) += x*y, carry into hi32. The carry-out lane mask goes through an SGPR pair the compiler
+// allocates (an early-clobber output), never VCC: a "vcc" clobber is not a reliable way to keep the
+// compiler from holding a live branch condition in VCC across the statement (seen on ROCm 7.2 in the
+// scalar-branch exponentiation loop).
+#define DH_MAC(acc, hi, x, y)                                                                       \
+  do {                                                                                              \
+    uint64_t c_;                                                                                    \
+    asm volatile("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_addc_co_u32_e64 %1, %2, 0, %1, %2"          \
+                 : "+v"(acc), "+v"(hi), "=&s"(c_)                                                   \
+                 : "v"(x), "v"(y));                                                                 \
+  } while (0)
 
 __device__ __forceinline__ void fips_mont_mul(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
   constexpr uint32_t P[12] = {0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u,
@@ -84,13 +89,13 @@ __device__ __forceinline__ void fips_mont_sqr(uint32_t r[12], const uint32_t a[1
     {
       uint32_t slo = (uint32_t)s, shi = (uint32_t)(s >> 32);
       uint32_t alo = (uint32_t)acc, ahi = (uint32_t)(acc >> 32);
+      uint64_t c_;
       asm volatile(
-          "v_add_co_u32_e32 %0, vcc, %0, %3\n\t"
-          "v_addc_co_u32_e32 %1, vcc, %1, %4, vcc\n\t"
-          "v_addc_co_u32_e32 %2, vcc, %2, %5, vcc"
-          : "+v"(alo), "+v"(ahi), "+v"(hi)
-          : "v"(slo), "v"(shi), "v"(sh)
-          : "vcc");
+          "v_add_co_u32_e64 %0, %3, %0, %4\n\t"
+          "v_addc_co_u32_e64 %1, %3, %1, %5, %3\n\t"
+          "v_addc_co_u32_e64 %2, %3, %2, %6, %3"
+          : "+v"(alo), "+v"(ahi), "+v"(hi), "=&s"(c_)
+          : "v"(slo), "v"(shi), "v"(sh));
       acc = (uint64_t)alo | ((uint64_t)ahi << 32);
     }
     if (k < 12) {
@@ -120,4 +125,56 @@ __device__ __forceinline__ void fips_mont_sqr(uint32_t r[12], const uint32_t a[1
 }
 
 #undef DH_MAC
+
+// The same product-scanning schedule in plain C (no inline asm): the carry-out of each 64-bit
+// accumulation is recovered with a compare, which the compiler fuses into v_cmp + v_addc. Kept as the
+// hazard-free reference for the asm version (bench/microbench_fp.hip compares both).
+#define DH_MACC(acc, hi, x, y)                             \
+  do {                                                     \
+    uint64_t t_ = (uint64_t)(x) * (uint64_t)(y) + (acc);   \
+    hi += t_ < (acc) ? 1u : 0u;                            \
+    acc = t_;                                              \
+  } while (0)
+
+__device__ __forceinline__ void fips_mont_mul_c(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
+  constexpr uint32_t P[12] = {0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u,
+                              0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau};
+  constexpr uint32_t NP0 = 0xfffcfffdu;
+  uint32_t m[12];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 12; k++) {
+#pragma unroll
+    for (int i = 0; i <= k; i++) DH_MACC(acc, hi, a[i], b[k - i]);
+#pragma unroll
+    for (int i = 0; i < k; i++) DH_MACC(acc, hi, m[i], P[k - i]);
+    m[k] = (uint32_t)acc * NP0;
+    DH_MACC(acc, hi, m[k], P[0]);
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int k = 12; k < 23; k++) {
+#pragma unroll
+    for (int i = k - 11; i < 12; i++) DH_MACC(acc, hi, a[i], b[k - i]);
+#pragma unroll
+    for (int i = k - 11; i < 12; i++) DH_MACC(acc, hi, m[i], P[k - i]);
+    r[k - 12] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  r[11] = (uint32_t)acc;
+  uint32_t d[12];
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)r[i] - P[i] - br;
+    d[i] = (uint32_t)t;
+    br = (t >> 63) & 1;
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) r[i] = br ? r[i] : d[i];
+}
+#undef DH_MACC
 }  // namespace dh

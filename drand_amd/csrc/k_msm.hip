@@ -1,0 +1,293 @@
+// Grouped Pippenger MSM for the random-linear-combination batch check (gfx950).
+#include "kcommon.hpp"
+
+namespace dh {
+
+// ---------------------------------------------------------------- grouped Pippenger MSM
+DH_DEV uint32_t scalar_digit(const uint4& s, int bit, int c) {
+  // bits [bit, bit + c) of the 128-bit little-endian scalar, zero beyond bit 127
+  const uint32_t w[4] = {s.x, s.y, s.z, s.w};
+  int wi = bit >> 5, sh = bit & 31;
+  uint64_t lo = wi < 4 ? w[wi] : 0;
+  uint64_t hi = wi + 1 < 4 ? w[wi + 1] : 0;
+  uint64_t v = (lo | (hi << 32)) >> sh;
+  return (uint32_t)v & ((1u << c) - 1);
+}
+
+// Entry e refers to point pidx[e] with scalar scal[sidx ? sidx[e] : pidx[e]] and belongs to group
+// grp ? grp[e] : e / gsize. The sorted list stores point indices, bucket by bucket.
+DH_DEV size_t entry_group(const uint32_t* grp, size_t e, uint32_t gsize) { return grp ? grp[e] : e / gsize; }
+
+__global__ void k_msm_hist(const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ sidx,
+                           const uint32_t* __restrict__ grp, size_t m, const uint4* __restrict__ scal, msm_geom g,
+                           uint32_t* __restrict__ cnt) {
+  size_t e = gtid();
+  if (e >= m) return;
+  const uint4 s = scal[sidx ? sidx[e] : pidx[e]];
+  const size_t gi = entry_group(grp, e, g.gsize);
+  for (int w = 0; w < g.nwin; w++) {
+    uint32_t d = scalar_digit(s, w * g.c, g.c);
+    if (d) atomicAdd(&cnt[(gi * g.nwin + w) * g.nbuck + d], 1u);
+  }
+}
+
+__global__ void k_msm_scatter(const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ sidx,
+                              const uint32_t* __restrict__ grp, size_t m, const uint4* __restrict__ scal, msm_geom g,
+                              uint32_t* __restrict__ cursor, uint32_t* __restrict__ list) {
+  size_t e = gtid();
+  if (e >= m) return;
+  const uint32_t idx = pidx[e];
+  const uint4 s = scal[sidx ? sidx[e] : idx];
+  const size_t gi = entry_group(grp, e, g.gsize);
+  for (int w = 0; w < g.nwin; w++) {
+    uint32_t d = scalar_digit(s, w * g.c, g.c);
+    if (d) {
+      uint32_t pos = atomicAdd(&cursor[(gi * g.nwin + w) * g.nbuck + d], 1u);
+      list[pos] = idx;
+    }
+  }
+}
+
+// exclusive scan, 3 phases: per-block totals, scan of totals (one block), final per-block scan
+constexpr int SCAN_T = 256, SCAN_I = 16, SCAN_B = SCAN_T * SCAN_I;
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const uint32_t* __restrict__ in, size_t n,
+                                                        uint32_t* __restrict__ block_sums) {
+  __shared__ uint32_t sh[SCAN_T];
+  size_t base = (size_t)blockIdx.x * SCAN_B + threadIdx.x * SCAN_I;
+  uint32_t s = 0;
+  for (int k = 0; k < SCAN_I; k++)
+    if (base + k < n) s += in[base + k];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = SCAN_T / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = sh[0];
+}
+
+// in-place exclusive scan of a[0..n) with n <= SCAN_B, single block; also writes the total to *total
+__global__ __launch_bounds__(SCAN_T) void k_scan_small(uint32_t* __restrict__ a, size_t n, uint32_t* __restrict__ total) {
+  __shared__ uint32_t sh[SCAN_T];
+  uint32_t v[SCAN_I];
+  size_t base = threadIdx.x * SCAN_I;
+  uint32_t s = 0;
+  for (int k = 0; k < SCAN_I; k++) {
+    v[k] = base + k < n ? a[base + k] : 0;
+    s += v[k];
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  // Hillis-Steele inclusive scan of the per-thread sums
+  for (int off = 1; off < SCAN_T; off <<= 1) {
+    uint32_t t = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += t;
+    __syncthreads();
+  }
+  uint32_t run = sh[threadIdx.x] - s;
+  for (int k = 0; k < SCAN_I; k++) {
+    if (base + k < n) a[base + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == SCAN_T - 1 && total) *total = sh[SCAN_T - 1];
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restrict__ in, size_t n,
+                                                       const uint32_t* __restrict__ block_off, uint32_t* __restrict__ out) {
+  __shared__ uint32_t sh[SCAN_T];
+  size_t base = (size_t)blockIdx.x * SCAN_B + threadIdx.x * SCAN_I;
+  uint32_t v[SCAN_I];
+  uint32_t s = 0;
+  for (int k = 0; k < SCAN_I; k++) {
+    v[k] = base + k < n ? in[base + k] : 0;
+    s += v[k];
+  }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < SCAN_T; off <<= 1) {
+    uint32_t t = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += t;
+    __syncthreads();
+  }
+  uint32_t run = block_off[blockIdx.x] + sh[threadIdx.x] - s;
+  for (int k = 0; k < SCAN_I; k++) {
+    if (base + k < n) out[base + k] = run;
+    run += v[k];
+  }
+}
+
+// bucket accumulation: one thread per (group, window, digit) key. P = affine (madd) or Jacobian (add) inputs.
+template <class F, bool AFFINE>
+__global__ __launch_bounds__(256, 4) void k_msm_bucket(const uint32_t* __restrict__ off, const uint32_t* __restrict__ list,
+                                                    size_t nkeys, const uint32_t* __restrict__ pts,
+                                                    uint32_t* __restrict__ buckets) {
+  size_t k = gtid();
+  if (k >= nkeys) return;
+  uint32_t b = off[k], e = off[k + 1];
+  jac<F> acc = jac_inf<F>();
+  for (uint32_t j = b; j < e; j++) {
+    uint32_t idx = list[j];
+    if constexpr (AFFINE) {
+      acc = jac_add_aff(acc, ld_aff_aos<F>(pts, idx));
+    } else {
+      acc = jac_add(acc, ld_jac_aos<F>(pts, idx));
+    }
+  }
+  st_jac_aos<F>(buckets, k, acc);
+}
+
+// per (group, window, segment): sum_{d in seg} d * B_d via running sums; seg covers digits [a, a + len)
+template <class F>
+__global__ __launch_bounds__(256, 4) void k_msm_segsum(const uint32_t* __restrict__ buckets, msm_geom g, size_t ngw,
+                                                    uint32_t* __restrict__ segs) {
+  size_t t = gtid();
+  if (t >= ngw * g.nseg) return;
+  const size_t gw = t / g.nseg;
+  const uint32_t s = t % g.nseg;
+  const uint32_t a = 1 + s * g.seglen;  // first digit of the segment
+  uint32_t last = a + g.seglen;         // exclusive
+  if (last > g.nbuck) last = g.nbuck;
+  jac<F> run = jac_inf<F>(), tot = jac_inf<F>();
+  for (int d = (int)last - 1; d >= (int)a; d--) {
+    run = jac_add(run, ld_jac_aos<F>(buckets, gw * g.nbuck + d));
+    tot = jac_add(tot, run);
+  }
+  // tot = sum (d - a + 1) B_d ; add (a - 1) * run
+  uint32_t k = a - 1;
+  if (k && !jac_is_inf(run)) {
+    jac<F> acc = jac_inf<F>();
+    for (int bit = 31 - __builtin_clz(k); bit >= 0; bit--) {
+      acc = jac_dbl(acc);
+      if ((k >> bit) & 1) acc = jac_add(acc, run);
+    }
+    tot = jac_add(tot, acc);
+  }
+  st_jac_aos<F>(segs, t, tot);
+}
+
+// pairwise tree reduction in place over rows of `stride` points whose first `width` are live:
+// v[r][c] += v[r][c + half] for c + half < width
+template <class F>
+__global__ __launch_bounds__(256, 4) void k_msm_tree(uint32_t* __restrict__ v, size_t rows, uint32_t stride, uint32_t width,
+                                                  uint32_t half) {
+  size_t t = gtid();
+  if (t >= rows * half) return;
+  size_t r = t / half, c = t % half;
+  if (c + half >= width) return;
+  size_t i = r * stride + c;
+  st_jac_aos<F>(v, i, jac_add(ld_jac_aos<F>(v, i), ld_jac_aos<F>(v, i + half)));
+}
+
+// per group: Horner over windows, result[g] = sum_w 2^(c w) W_{g,w}; W_{g,w} = segs[(g*nwin + w) * nseg]
+template <class F>
+__global__ __launch_bounds__(64) void k_msm_windows(const uint32_t* __restrict__ segs, msm_geom g, size_t ngroups,
+                                                    uint32_t* __restrict__ out) {
+  size_t t = gtid();
+  if (t >= ngroups) return;
+  jac<F> acc = ld_jac_aos<F>(segs, (t * g.nwin + g.nwin - 1) * g.nseg);
+  for (int w = g.nwin - 2; w >= 0; w--) {
+    for (int k = 0; k < g.c; k++) acc = jac_dbl(acc);
+    acc = jac_add(acc, ld_jac_aos<F>(segs, (t * g.nwin + w) * g.nseg));
+  }
+  st_jac_aos<F>(out, t, acc);
+}
+
+
+__global__ void k_mark_groups(const uint32_t* __restrict__ entries, size_t m, size_t gsize, const uint8_t* __restrict__ pass,
+                              const uint8_t* __restrict__ status, uint8_t* __restrict__ verdict) {
+  size_t e = gtid();
+  if (e >= m) return;
+  uint32_t i = entries[e];
+  if (pass[e / gsize]) verdict[i] = status[i] == DEC_OK ? 1 : 0;
+}
+
+__global__ void k_iota(uint32_t* __restrict__ v, size_t n) {
+  size_t i = gtid();
+  if (i < n) v[i] = (uint32_t)i;
+}
+
+
+hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_iota, dim3(nblk(n, 256)), dim3(256), 0, st, v, n);
+  return hipGetLastError();
+}
+
+// exclusive scan of cnt[0..nk) into off[0..nk], off[nk] = total; tmp needs nblk(nk, SCAN_B) words
+
+hipError_t launch_scan(const uint32_t* cnt, size_t nk, uint32_t* off, uint32_t* tmp, hipStream_t st) {
+  size_t nb = (nk + SCAN_B - 1) / SCAN_B;
+  if (nb > (size_t)SCAN_B) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(SCAN_T), 0, st, cnt, nk, tmp);
+  hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SCAN_T), 0, st, tmp, nb, off + nk);
+  hipLaunchKernelGGL(k_scan_final, dim3((unsigned)nb), dim3(SCAN_T), 0, st, cnt, nk, tmp, off);
+  return hipGetLastError();
+}
+
+
+template <class F>
+static hipError_t msm_reduce(const msm_geom& g, size_t ngroups, uint32_t* buckets, uint32_t* segs, uint32_t* out,
+                             hipStream_t st) {
+  size_t ngw = ngroups * g.nwin;
+  hipLaunchKernelGGL(k_msm_segsum<F>, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, buckets, g, ngw, segs);
+  for (uint32_t width = g.nseg; width > 1;) {
+    uint32_t half = (width + 1) / 2;
+    hipLaunchKernelGGL(k_msm_tree<F>, dim3(nblk(ngw * half, 256)), dim3(256), 0, st, segs, ngw, g.nseg, width, half);
+    width = half;  // live prefix of each row; the row stride stays nseg
+  }
+  hipLaunchKernelGGL(k_msm_windows<F>, dim3(nblk(ngroups, 64)), dim3(64), 0, st, segs, g, ngroups, out);
+  return hipGetLastError();
+}
+
+
+hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp, size_t m,
+                           size_t ngroups, const uint4* scal, msm_ws& ws, hipStream_t st) {
+  size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
+  hipError_t e = hipMemsetAsync(ws.cnt, 0, nk * sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  if (m) hipLaunchKernelGGL(k_msm_hist, dim3(nblk(m, 256)), dim3(256), 0, st, pidx, sidx, grp, m, scal, g, ws.cnt);
+  if ((e = launch_scan(ws.cnt, nk, ws.off, ws.scan_tmp, st)) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(ws.cnt, ws.off, nk * sizeof(uint32_t), hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
+  if (m) hipLaunchKernelGGL(k_msm_scatter, dim3(nblk(m, 256)), dim3(256), 0, st, pidx, sidx, grp, m, scal, g, ws.cnt, ws.list);
+  return hipGetLastError();
+}
+
+// point set of the sorted lists: field (G1 / G2) and representation (affine AoS / Jacobian AoS)
+hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngroups, const uint32_t* pts, msm_ws& ws,
+                             uint32_t* out, hipStream_t st) {
+  size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
+  if (g2) {
+    if (affine)
+      hipLaunchKernelGGL((k_msm_bucket<fp2, true>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, pts, ws.buckets);
+    else
+      hipLaunchKernelGGL((k_msm_bucket<fp2, false>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, pts, ws.buckets);
+    return msm_reduce<fp2>(g, ngroups, ws.buckets, ws.segs, out, st);
+  }
+  if (affine)
+    hipLaunchKernelGGL((k_msm_bucket<fp, true>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, pts, ws.buckets);
+  else
+    hipLaunchKernelGGL((k_msm_bucket<fp, false>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, pts, ws.buckets);
+  return msm_reduce<fp>(g, ngroups, ws.buckets, ws.segs, out, st);
+}
+
+hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
+                      const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
+                      hipStream_t st) {
+  hipError_t e = launch_msm_sort(g, entries, nullptr, nullptr, m, ngroups, scal, ws, st);
+  if (e != hipSuccess) return e;
+  if ((e = launch_msm_points(sig_g2, 1, g, ngroups, sig_aff, ws, outA, st)) != hipSuccess) return e;
+  return launch_msm_points(sig_g2, 0, g, ngroups, q_pts, ws, outB, st);
+}
+
+hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,
+                              uint8_t* verdict, hipStream_t st) {
+  if (!m) return hipSuccess;
+  hipLaunchKernelGGL(k_mark_groups, dim3(nblk(m, 256)), dim3(256), 0, st, entries, m, gsize, pass, status, verdict);
+  return hipGetLastError();
+}
+
+
+}  // namespace dh

@@ -1,0 +1,246 @@
+// Threshold-BLS Recover on gfx950: kyber v1.1.18 sign/tbls Recover + share.RecoverCommit as called at
+// /root/reference/chain/beacon/chainstore.go:202 (then VerifyRecovered at :207), batched over rounds.
+//
+//   k_repack_partials   (2-byte BE index || sig) records -> aligned signatures + share indices
+//   k_pubpoly_eval      PubPoly.Eval(i) = sum_j C_j (i+1)^j for every signer index (Horner, small scalars)
+//   [partial signatures decoded by k_prep_sig, hash points by k_prep_msg32, RLC scalars by k_scalars]
+//   batch VerifyPartial: sum_{j,i} r_ji sigma_ji  vs  per signer i: [h] sum_j r_ji Q_j  (grouped MSM), then
+//   k_pair_miller       one lane per pair of the multi-pairing prod_i e(pk_i, B_i) e(-g, A) -> Miller value
+//   k_pair_product      one lane: product of the Miller values, final exponentiation, == 1
+//   k_partial_leaf      per-partial VerifyPartial (only when the batch check fails)
+//   k_lagrange          per round: sum_k lambda_k sigma_k (Straus, shared doublings), lambda from the host
+//   k_compress          recovered signatures -> compressed bytes
+#include "kcommon.hpp"
+
+namespace dh {
+
+__global__ void k_repack_partials(const uint8_t* __restrict__ raw, size_t n, int sig_len, uint8_t* __restrict__ sigs,
+                                  uint32_t* __restrict__ idx) {
+  size_t i = gtid();
+  if (i >= n) return;
+  const uint8_t* r = raw + i * (size_t)(2 + sig_len);
+  idx[i] = ((uint32_t)r[0] << 8) | r[1];
+  uint32_t* o = (uint32_t*)(sigs + i * (size_t)sig_len);
+  for (int w = 0; w < sig_len / 4; w++) {
+    const uint8_t* q = r + 2 + 4 * w;
+    o[w] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  }
+}
+
+// commits: t affine key-group points (AoS); out[i] = Eval(i) Jacobian, x = i + 1
+template <class K>
+__global__ void k_pubpoly_eval(const uint32_t* __restrict__ commits, int t, int n_nodes, uint32_t* __restrict__ out) {
+  size_t i = gtid();
+  if (i >= (size_t)n_nodes) return;
+  const uint32_t x = (uint32_t)i + 1;
+  jac<K> acc = jac_from_aff(ld_aff_aos<K>(commits, t - 1));
+  for (int j = t - 2; j >= 0; j--) {
+    // acc = [x] acc + C_j
+    jac<K> base = acc, r = jac_inf<K>();
+    for (int b = 31 - __builtin_clz(x); b >= 0; b--) {
+      r = jac_dbl(r);
+      if ((x >> b) & 1) r = jac_add(r, base);
+    }
+    acc = jac_add_aff(r, ld_aff_aos<K>(commits, j));
+  }
+  st_jac_aos<K>(out, i, acc);
+}
+
+// Miller loop of one pair per lane. P side G1, Q side G2 (Jacobian AoS arrays); cofactor clearing of the
+// hash side is applied here (clear_p / clear_q); neg_p negates P. Output: fp12 Miller value, skip flag.
+__global__ __launch_bounds__(64) void k_pair_miller(const uint32_t* __restrict__ P, const uint32_t* __restrict__ Q,
+                                                    size_t npairs, int clear_p, int clear_q, const uint8_t* __restrict__ live,
+                                                    uint32_t* __restrict__ f_out, uint8_t* __restrict__ skip_out) {
+  size_t i = gtid();
+  if (i >= npairs) return;
+  jac<fp> p = ld_jac_aos<fp>(P, i);
+  jac<fp2> q = ld_jac_aos<fp2>(Q, i);
+  if (clear_p) p = h2c_clear_g1(p);
+  if (clear_q) q = h2c_clear_g2(q);
+  bool skip = jac_is_inf(p) || jac_is_inf(q) || (live && !live[i]);
+  fp12 f = fp12_one();
+  if (!skip) {
+    aff<fp> pa[1] = {jac_to_aff(p)};
+    aff<fp2> qa[1] = {jac_to_aff(q)};
+    bool sk[1] = {false};
+    f = miller_loop<1>(pa, qa, sk);
+  }
+  uint32_t* o = f_out + i * 144;
+  const fp2* c = &f.c0.c0;
+  for (int k = 0; k < 6; k++) {
+    st_f<fp2>(o + 24 * k, c[k]);
+  }
+  skip_out[i] = skip ? 1 : 0;
+}
+
+__global__ void k_pair_product(const uint32_t* __restrict__ f_in, const uint8_t* __restrict__ skip, size_t npairs,
+                               uint8_t* __restrict__ pass) {
+  if (gtid() != 0) return;
+  fp12 acc = fp12_one();
+  for (size_t i = 0; i < npairs; i++) {
+    if (skip[i]) continue;
+    fp12 f;
+    fp2* c = &f.c0.c0;
+    for (int k = 0; k < 6; k++) ld_f<fp2>(c[k], f_in + i * 144 + 24 * k);
+    acc = fp12_mul(acc, f);
+  }
+  *pass = fp12_is_one(final_exp(acc)) ? 1 : 0;
+}
+
+// VerifyPartial for each listed partial e: pubshare = shares[idx[e]], hash point q[round_of[e]]
+template <class F>
+__global__ __launch_bounds__(64) void k_partial_leaf(const uint32_t* __restrict__ list, size_t m,
+                                                     const uint32_t* __restrict__ sig_aff, const uint8_t* __restrict__ status,
+                                                     const uint32_t* __restrict__ share_idx,
+                                                     const uint32_t* __restrict__ round_of, const uint32_t* __restrict__ q_pts,
+                                                     const uint32_t* __restrict__ shares, int n_nodes,
+                                                     uint8_t* __restrict__ ok_out) {
+  size_t t = gtid();
+  if (t >= m) return;
+  const uint32_t e = list[t];
+  const uint32_t si = share_idx[e];
+  if (status[e] != DEC_OK || si >= (uint32_t)n_nodes) {
+    ok_out[e] = 0;
+    return;
+  }
+  jac<F> S = jac_from_aff(ld_aff_aos<F>(sig_aff, e));
+  bool ok;
+  if constexpr (sizeof(F) == sizeof(fp2)) {
+    jac<fp2> H = h2c_clear_g2(ld_jac_aos<fp2>(q_pts, round_of[e]));
+    jac<fp> pk = ld_jac_aos<fp>(shares, si);
+    jac<fp> Pp[2] = {pk, jac_neg(g1_gen())};
+    jac<fp2> Qq[2] = {H, S};
+    ok = pairing_check<2>(Pp, Qq);
+  } else {
+    jac<fp> H = h2c_clear_g1(ld_jac_aos<fp>(q_pts, round_of[e]));
+    jac<fp2> pk = ld_jac_aos<fp2>(shares, si);
+    jac<fp> Pp[2] = {H, jac_neg(S)};
+    jac<fp2> Qq[2] = {pk, g2_gen()};
+    ok = pairing_check<2>(Pp, Qq);
+  }
+  ok_out[e] = ok ? 1 : 0;
+}
+
+// sigma_j = sum_k lambda_{j,k} sigma_{sel[j,k]}: Straus over t points with shared doublings.
+// lam: nsets x t x 8 words (little-endian 256-bit scalars mod r); lam_set[j] selects the row set.
+template <class F>
+__global__ __launch_bounds__(64) void k_lagrange(const uint32_t* __restrict__ sel, const uint32_t* __restrict__ lam,
+                                                 const uint32_t* __restrict__ lam_set, const uint8_t* __restrict__ ok,
+                                                 int t, size_t n_rounds, const uint32_t* __restrict__ sig_aff,
+                                                 uint32_t* __restrict__ out) {
+  size_t j = gtid();
+  if (j >= n_rounds) return;
+  jac<F> acc = jac_inf<F>();
+  if (ok[j]) {
+    const uint32_t* L = lam + (size_t)lam_set[j] * t * 8;
+    const uint32_t* S = sel + j * (size_t)t;
+    for (int b = 254; b >= 0; b--) {
+      acc = jac_dbl(acc);
+      for (int k = 0; k < t; k++) {
+        if ((L[k * 8 + (b >> 5)] >> (b & 31)) & 1) acc = jac_add_aff(acc, ld_aff_aos<F>(sig_aff, S[k]));
+      }
+    }
+  }
+  st_jac_aos<F>(out, j, acc);
+}
+
+template <class F>
+__global__ __launch_bounds__(64) void k_compress(const uint32_t* __restrict__ pts, size_t n, uint8_t* __restrict__ out) {
+  size_t j = gtid();
+  if (j >= n) return;
+  jac<F> p = ld_jac_aos<F>(pts, j);
+  if constexpr (sizeof(F) == sizeof(fp)) g1_compress(out + 48 * j, p);
+  else g2_compress(out + 96 * j, p);
+}
+
+// assemble the pairs of the batched VerifyPartial check:
+//   G2 signatures: (share_i, [h] B_i) for i < n_nodes, then (-g1, A)
+//   G1 signatures: ([h] B_i, share_i) for i < n_nodes, then (-A, g2)
+template <class F>
+__global__ __launch_bounds__(64) void k_recover_pairs(const uint32_t* __restrict__ shares, const uint32_t* __restrict__ B,
+                                                      const uint32_t* __restrict__ A, int n_nodes,
+                                                      uint32_t* __restrict__ P, uint32_t* __restrict__ Q) {
+  size_t i = gtid();
+  if (i > (size_t)n_nodes) return;
+  if constexpr (sizeof(F) == sizeof(fp2)) {
+    if (i < (size_t)n_nodes) {
+      st_jac_aos<fp>(P, i, ld_jac_aos<fp>(shares, i));
+      st_jac_aos<fp2>(Q, i, h2c_clear_g2(ld_jac_aos<fp2>(B, i)));
+    } else {
+      st_jac_aos<fp>(P, i, jac_neg(g1_gen()));
+      st_jac_aos<fp2>(Q, i, ld_jac_aos<fp2>(A, 0));
+    }
+  } else {
+    if (i < (size_t)n_nodes) {
+      st_jac_aos<fp>(P, i, h2c_clear_g1(ld_jac_aos<fp>(B, i)));
+      st_jac_aos<fp2>(Q, i, ld_jac_aos<fp2>(shares, i));
+    } else {
+      st_jac_aos<fp>(P, i, jac_neg(ld_jac_aos<fp>(A, 0)));
+      st_jac_aos<fp2>(Q, i, g2_gen());
+    }
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_repack_partials(const uint8_t* raw, size_t n, int sig_len, uint8_t* sigs, uint32_t* idx, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_repack_partials, dim3(nblk(n, 256)), dim3(256), 0, st, raw, n, sig_len, sigs, idx);
+  return hipGetLastError();
+}
+
+hipError_t launch_pubpoly_eval(int key_g2, const uint32_t* commits, int t, int n_nodes, uint32_t* out, hipStream_t st) {
+  if (key_g2) hipLaunchKernelGGL(k_pubpoly_eval<fp2>, dim3(nblk(n_nodes, 64)), dim3(64), 0, st, commits, t, n_nodes, out);
+  else hipLaunchKernelGGL(k_pubpoly_eval<fp>, dim3(nblk(n_nodes, 64)), dim3(64), 0, st, commits, t, n_nodes, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pair_check(const uint32_t* P, const uint32_t* Q, size_t npairs, int clear_p, int clear_q,
+                             const uint8_t* live, uint32_t* f_tmp, uint8_t* skip_tmp, uint8_t* pass, hipStream_t st) {
+  hipLaunchKernelGGL(k_pair_miller, dim3(nblk(npairs, 64)), dim3(64), 0, st, P, Q, npairs, clear_p, clear_q, live, f_tmp,
+                     skip_tmp);
+  hipLaunchKernelGGL(k_pair_product, dim3(1), dim3(64), 0, st, f_tmp, skip_tmp, npairs, pass);
+  return hipGetLastError();
+}
+
+hipError_t launch_partial_leaf(int sig_g2, const uint32_t* list, size_t m, const uint32_t* sig_aff, const uint8_t* status,
+                               const uint32_t* share_idx, const uint32_t* round_of, const uint32_t* q_pts,
+                               const uint32_t* shares, int n_nodes, uint8_t* ok_out, hipStream_t st) {
+  if (!m) return hipSuccess;
+  if (sig_g2)
+    hipLaunchKernelGGL(k_partial_leaf<fp2>, dim3(nblk(m, 64)), dim3(64), 0, st, list, m, sig_aff, status, share_idx, round_of,
+                       q_pts, shares, n_nodes, ok_out);
+  else
+    hipLaunchKernelGGL(k_partial_leaf<fp>, dim3(nblk(m, 64)), dim3(64), 0, st, list, m, sig_aff, status, share_idx, round_of,
+                       q_pts, shares, n_nodes, ok_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
+                           int t, size_t n_rounds, const uint32_t* sig_aff, uint32_t* out, hipStream_t st) {
+  if (!n_rounds) return hipSuccess;
+  if (sig_g2)
+    hipLaunchKernelGGL(k_lagrange<fp2>, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, sel, lam, lam_set, ok, t, n_rounds, sig_aff,
+                       out);
+  else
+    hipLaunchKernelGGL(k_lagrange<fp>, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, sel, lam, lam_set, ok, t, n_rounds, sig_aff,
+                       out);
+  return hipGetLastError();
+}
+
+hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, hipStream_t st) {
+  if (!n) return hipSuccess;
+  if (sig_g2) hipLaunchKernelGGL(k_compress<fp2>, dim3(nblk(n, 64)), dim3(64), 0, st, pts, n, out);
+  else hipLaunchKernelGGL(k_compress<fp>, dim3(nblk(n, 64)), dim3(64), 0, st, pts, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_recover_pairs(int sig_g2, const uint32_t* shares, const uint32_t* B, const uint32_t* A, int n_nodes,
+                                uint32_t* P, uint32_t* Q, hipStream_t st) {
+  if (sig_g2)
+    hipLaunchKernelGGL(k_recover_pairs<fp2>, dim3(nblk(n_nodes + 1, 64)), dim3(64), 0, st, shares, B, A, n_nodes, P, Q);
+  else
+    hipLaunchKernelGGL(k_recover_pairs<fp>, dim3(nblk(n_nodes + 1, 64)), dim3(64), 0, st, shares, B, A, n_nodes, P, Q);
+  return hipGetLastError();
+}
+
+}  // namespace dh

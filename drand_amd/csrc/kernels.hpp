@@ -32,6 +32,7 @@ hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n,
                        uint8_t* rand_out, hipStream_t st);
 hipError_t launch_msg(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
                       size_t n, int chained, int dst_id, uint32_t* q_out, hipStream_t st);
+hipError_t launch_msg32(int sig_g2, const uint8_t* msgs, size_t n, int dst_id, uint32_t* q_out, hipStream_t st);
 hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, hipStream_t st);
 hipError_t launch_decode_key(int key_g2, const uint8_t* pk, uint32_t* key_aff, uint8_t* ok, hipStream_t st);
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t st);
@@ -39,6 +40,10 @@ hipError_t launch_scan(const uint32_t* cnt, size_t nk, uint32_t* off, uint32_t* 
 hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
                       const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
                       hipStream_t st);
+hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp, size_t m,
+                           size_t ngroups, const uint4* scal, msm_ws& ws, hipStream_t st);
+hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngroups, const uint32_t* pts, msm_ws& ws,
+                             uint32_t* out, hipStream_t st);
 hipError_t launch_group_check(int sig_g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_aff,
                               uint8_t* pass, hipStream_t st);
 hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,
@@ -49,5 +54,19 @@ hipError_t launch_leaf_check(int sig_g2, const uint32_t* entries, size_t m, cons
 hipError_t launch_sign(int sig_g2, const uint32_t* sk, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride,
                        const uint32_t* prev_lens, size_t n, int chained, int dst_id, uint8_t* out, hipStream_t st);
 hipError_t launch_pubkey(int key_g2, const uint32_t* sk, uint8_t* out, hipStream_t st);
+
+// tbls Recover (k_recover.hip)
+hipError_t launch_repack_partials(const uint8_t* raw, size_t n, int sig_len, uint8_t* sigs, uint32_t* idx, hipStream_t st);
+hipError_t launch_pubpoly_eval(int key_g2, const uint32_t* commits, int t, int n_nodes, uint32_t* out, hipStream_t st);
+hipError_t launch_pair_check(const uint32_t* P, const uint32_t* Q, size_t npairs, int clear_p, int clear_q,
+                             const uint8_t* live, uint32_t* f_tmp, uint8_t* skip_tmp, uint8_t* pass, hipStream_t st);
+hipError_t launch_partial_leaf(int sig_g2, const uint32_t* list, size_t m, const uint32_t* sig_aff, const uint8_t* status,
+                               const uint32_t* share_idx, const uint32_t* round_of, const uint32_t* q_pts,
+                               const uint32_t* shares, int n_nodes, uint8_t* ok_out, hipStream_t st);
+hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
+                           int t, size_t n_rounds, const uint32_t* sig_aff, uint32_t* out, hipStream_t st);
+hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, hipStream_t st);
+hipError_t launch_recover_pairs(int sig_g2, const uint32_t* shares, const uint32_t* B, const uint32_t* A, int n_nodes,
+                                uint32_t* P, uint32_t* Q, hipStream_t st);
 
 }  // namespace dh

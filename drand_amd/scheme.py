@@ -99,6 +99,44 @@ class Scheme:
                                            _ptr(prev), pstride, _ptr(plen), n, _ptr(verdict), _ptr(rand), int(seed)))
         return verdict.astype(bool), rand
 
+    # ---- threshold BLS (kyber sign/tbls as used at chain/beacon/chainstore.go:202,207)
+    def recover_batch(self, commits, t, n, msgs, partials_per_round):
+        """Batch tbls Recover. commits: t compressed key-group points (PubPoly commits, index 0 = group key);
+        msgs: per-round 32-byte messages (DigestBeacon); partials_per_round: per round a list of
+        (2-byte BE share index || signature) records, in arrival order.
+        Returns (signatures (n_rounds, sig_len) uint8, ok (n_rounds,) bool) where ok[j] is False when
+        fewer than t valid partials were given (Go: "not enough good public shares")."""
+        commits = b"".join(bytes(c) for c in commits)
+        if len(commits) != t * self.key_len:
+            raise SchemeError("need t commitments of %d bytes" % self.key_len)
+        n_rounds = len(msgs)
+        m = np.frombuffer(b"".join(bytes(x) for x in msgs), dtype=np.uint8).copy() if n_rounds else np.zeros(0, np.uint8)
+        if len(m) != 32 * n_rounds:
+            raise SchemeError("messages must be 32-byte digests")
+        rec = 2 + self.sig_len
+        off = np.zeros(n_rounds + 1, dtype=np.uint32)
+        blobs = []
+        for j, parts in enumerate(partials_per_round):
+            for p in parts:
+                p = bytes(p)
+                if len(p) != rec:
+                    raise SchemeError("partial signature must be %d bytes" % rec)
+                blobs.append(p)
+            off[j + 1] = len(blobs)
+        raw = np.frombuffer(b"".join(blobs), dtype=np.uint8).copy() if blobs else np.zeros(rec, np.uint8)
+        sigs = np.zeros((n_rounds, self.sig_len), dtype=np.uint8)
+        ok = np.zeros(n_rounds, dtype=np.uint8)
+        _check(_lib.load().dh_recover_batch(self.id, commits, int(t), int(n), _ptr(m), _ptr(raw), _ptr(off), n_rounds,
+                                            _ptr(sigs), _ptr(ok)))
+        return sigs, ok.astype(bool)
+
+    def recover(self, commits, msg, partials, t, n):
+        """ThresholdScheme.Recover(pubPoly, msg, sigs, t, n): the recovered signature, or SchemeError."""
+        sigs, ok = self.recover_batch(commits, t, n, [msg], [partials])
+        if not ok[0]:
+            raise SchemeError("not enough good public shares")
+        return sigs[0].tobytes()
+
     def randomness(self, signatures):
         sigs = np.ascontiguousarray(signatures, dtype=np.uint8)
         out = np.zeros((len(sigs), 32), dtype=np.uint8)

@@ -206,6 +206,44 @@ def cw(ws):
     return "{" + ", ".join("0x%08xu" % v for v in ws) + "}"
 
 
+def window_schedule(e, wbits):
+    """Left-to-right sliding window over odd digits < 2^wbits.
+    Returns [first_index, (nsq << 8) | idx, ...]; idx = (digit - 1) / 2, 0xff = squarings only."""
+    b = bin(e)[2:]
+    i = 0
+    ops = []
+    acc = None
+    pending_sq = 0
+    while i < len(b):
+        if b[i] == "0":
+            pending_sq += 1
+            i += 1
+            continue
+        j = min(i + wbits, len(b))
+        while b[j - 1] == "0":
+            j -= 1
+        digit = int(b[i:j], 2)
+        width = j - i
+        if acc is None:
+            ops.append((digit - 1) // 2)
+            acc = digit
+        else:
+            pending_sq += width
+            while pending_sq > 255:
+                ops.append((255 << 8) | 0xFF)
+                acc <<= 255
+                pending_sq -= 255
+            ops.append((pending_sq << 8) | ((digit - 1) // 2))
+            acc = (acc << pending_sq) + digit
+        pending_sq = 0
+        i = j
+    if pending_sq:
+        ops.append((pending_sq << 8) | 0xFF)
+        acc <<= pending_sq
+    assert acc == e
+    return ops
+
+
 def main():
     assert (P - 1) % 3 == 0 and P % 4 == 3
     xi = (1, 1)
@@ -301,6 +339,13 @@ def main():
         w("constexpr int %s_WORDS = %d;" % (name, n))
         w("constexpr int %s_BITS = %d;" % (name, e.bit_length()))
         w("__device__ __constant__ uint32_t %s[%d] = %s;" % (name, n, txt))
+    # sliding-window (w = 3, odd powers x^1,3,5,7) schedules for the fixed Fp exponents:
+    # entry = (squarings << 8) | table index, index 0xff = squarings only (trailing zeros)
+    for name, e in (("SCHED_SQRT", (P + 1) // 4), ("SCHED_SR1_C1", sr1_c1), ("SCHED_INV", P - 2),
+                    ("SCHED_LEGENDRE", (P - 1) // 2)):
+        sched = window_schedule(e, 3)
+        w("constexpr int %s_LEN = %d;" % (name, len(sched)))
+        w("__device__ __constant__ uint16_t %s[%d] = {%s};" % (name, len(sched), ", ".join("0x%04x" % v for v in sched)))
     w("constexpr uint32_t SR2_C4 = %du;" % c4)
     w("constexpr uint32_t SR2_C5 = %du;" % c5)
     w("constexpr int SR2_C1 = %d;" % c1)

@@ -118,6 +118,38 @@ def negatives(scheme, sk, pk, rng):
     return out
 
 
+def recover_fixture(scheme, t, n, rounds, rng):
+    """Dealer polynomial -> commits, shares; per round a list of partials in arrival order, some invalid,
+    expected outputs from the oracle's restatement of kyber tbls.Recover + share.RecoverCommit."""
+    coeffs = [int.from_bytes(hashlib.sha256(b"tbls-%s-%d" % (scheme.encode(), j)).digest(), "big") % R for j in range(t)]
+    commits = [orc.public_key(scheme, c.to_bytes(32, "big")) for c in coeffs]
+
+    def share(i):  # f(i + 1)
+        x, acc = i + 1, 0
+        for c in reversed(coeffs):
+            acc = (acc * x + c) % R
+        return acc.to_bytes(32, "big")
+
+    cases = []
+    for k, r in enumerate(rounds):
+        msg = orc.digest_beacon(scheme, r, b"")
+        ids = rng.sample(range(n), t + 2)
+        parts = [i.to_bytes(2, "big") + orc.sign(scheme, share(i), msg) for i in ids]
+        if k % 4 == 1:   # an invalid partial first: skipped, the t valid ones after it are used
+            bad = bytearray(parts[0]); bad[5] ^= 1; parts[0] = bytes(bad)
+        if k % 4 == 2:   # duplicate of an index and an out-of-range index
+            parts.insert(1, parts[0])
+            parts.insert(2, (n + 3).to_bytes(2, "big") + parts[3][2:])
+        if k % 4 == 3:   # too few valid partials -> error
+            parts = parts[: t - 1]
+        got = orc.recover(scheme, commits, t, n, msg, parts)
+        if got is not None:
+            assert got == orc.sign(scheme, coeffs[0].to_bytes(32, "big"), msg)
+        cases.append({"round": r, "msg": msg.hex(), "partials": [p.hex() for p in parts],
+                      "expected": got.hex() if got else None})
+    return {"t": t, "n": n, "commits": [c.hex() for c in commits], "group_key": commits[0].hex(), "cases": cases}
+
+
 def main():
     rng = random.Random(20250117)
     chains, negs = {}, {}
@@ -146,6 +178,10 @@ def main():
     assert faulty == [10, 11], faulty
     replay = {"pk": c["pk"], "rounds": c["rounds"], "stored_sigs": [s.hex() for s in stored],
               "genesis_seed": GENESIS_SEED.hex(), "faulty": faulty}
+    rec = {s_: recover_fixture(s_, 5, 9, list(range(100, 108)), rng)
+           for s_ in ("pedersen-bls-unchained", "bls-unchained-g1-rfc9380")}
+    with open(os.path.join(HERE, "recover.json"), "w") as f:
+        json.dump(rec, f, indent=1)
     with open(os.path.join(HERE, "chains.json"), "w") as f:
         json.dump(chains, f, indent=1)
     with open(os.path.join(HERE, "negatives.json"), "w") as f:

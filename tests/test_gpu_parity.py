@@ -140,3 +140,55 @@ def test_bad_key_and_arguments(dh):
         s.verify_beacons(b"\x00" * 95, [1], np.zeros((1, 48), np.uint8))
     v, _ = s.verify_beacons(VERIFY_KATS[3][1], [], np.zeros((0, 48), np.uint8))
     assert len(v) == 0
+
+
+@pytest.mark.parametrize("scheme", ["pedersen-bls-unchained", "bls-unchained-g1-rfc9380"])
+def test_recover_golden(dh, scheme):
+    """tbls Recover (chain/beacon/chainstore.go:202) vs the oracle: invalid partials skipped in arrival
+    order, duplicate / out-of-range indices, too few valid partials -> error."""
+    c = json.load(open(os.path.join(GOLD, "recover.json")))[scheme]
+    s = dh.scheme_from_name(scheme)
+    commits = [bytes.fromhex(x) for x in c["commits"]]
+    msgs = [bytes.fromhex(x["msg"]) for x in c["cases"]]
+    parts = [[bytes.fromhex(p) for p in x["partials"]] for x in c["cases"]]
+    sigs, ok = s.recover_batch(commits, c["t"], c["n"], msgs, parts)
+    for k, x in enumerate(c["cases"]):
+        if x["expected"] is None:
+            assert not ok[k], k
+        else:
+            assert ok[k], k
+            assert sigs[k].tobytes().hex() == x["expected"], k
+    with pytest.raises(dh.SchemeError):
+        s.recover(commits, msgs[3], parts[3], c["t"], c["n"])
+    assert s.recover(commits, msgs[0], parts[0], c["t"], c["n"]).hex() == c["cases"][0]["expected"]
+
+
+def test_recover_threshold_property(dh):
+    """n = 16 signers, t = 9, 40 rounds, random signer subsets per round (partials signed on the device):
+    the recovered signature equals [f(0)] H(m) and verifies under the group key (dealer pattern
+    /root/reference/chain/beacon/node_test.go:60-109)."""
+    import random
+    s = dh.scheme_from_name("pedersen-bls-unchained")
+    R = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    t, n, nr = 9, 16, 40
+    coeffs = [int.from_bytes(hashlib.sha256(b"prop-%d" % j).digest(), "big") % R for j in range(t)]
+    commits = [s.public_key(cf.to_bytes(32, "big")) for cf in coeffs]
+    rounds = np.arange(500, 500 + nr, dtype=np.uint64)
+    shares = []
+    for i in range(n):
+        x, acc = i + 1, 0
+        for cf in reversed(coeffs):
+            acc = (acc * x + cf) % R
+        shares.append(s.sign_beacons(acc.to_bytes(32, "big"), rounds))
+    rng = random.Random(7)
+    parts = []
+    for j in range(nr):
+        ids = rng.sample(range(n), t + rng.randrange(0, 3))
+        parts.append([i.to_bytes(2, "big") + shares[i][j].tobytes() for i in ids])
+    msgs = [s.digest_beacon(int(r)) for r in rounds]
+    sigs, ok = s.recover_batch(commits, t, n, msgs, parts)
+    assert ok.all()
+    want = s.sign_beacons(coeffs[0].to_bytes(32, "big"), rounds)
+    assert np.array_equal(sigs, want)
+    v, _ = s.verify_beacons(commits[0], rounds, sigs, seed=2)
+    assert v.all()
