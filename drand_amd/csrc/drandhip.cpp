@@ -8,7 +8,7 @@
 // Verification flow of one batch (dh_verify_batch_device):
 //   decode pk -> prep signatures (status, affine sigma, randomness) -> prep messages (Q_i, pre-cofactor)
 //   -> RLC scalars -> level 0: one group = every round: MSM + pairing check
-//   -> on failure, bisection levels with smaller groups (4096, 64 rounds) over the failing groups only
+//   -> on failure, bisection levels with smaller groups (4096, 256, 16, 2 rounds) over the failing groups only
 //   -> leaves: per-round 2-pairing checks. Verdict = decode ok AND (group passed OR leaf passed),
 //   which is the per-round VerifyBeacon verdict of /root/reference/crypto/schemes.go:70-72.
 #include <hip/hip_runtime.h>
@@ -86,7 +86,7 @@ struct worker {
   // key
   dbuf key_raw, key_aff, key_ok;
   // MSM
-  dbuf cnt, off, scan_tmp, list, buckets, segs, outA, outB, pass;
+  dbuf cnt, off, scan_tmp, list, buckets, segs, outA, outB, out2, pass;
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
@@ -101,7 +101,7 @@ struct worker {
   void release_all() {
     dbuf* all[] = {&status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
-                   &scan_tmp, &list, &buckets, &segs, &outA, &outB, &pass, &r_commits, &r_cstatus, &r_caff, &r_shares,
+                   &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
                    &r_sigbytes, &r_status2, &r_aff2, &r_entries2};
@@ -395,11 +395,12 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
   HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
 
-  // bisection levels: group sizes n, 4096, 64, then per-round leaves
+  // bisection levels: group sizes n, 4096, 256, 16, 2, then per-round leaves (a failing group is re-checked
+  // as smaller groups with the same scalars; only rounds of failing pairs reach a per-round pairing check)
   size_t m = n;
   std::vector<size_t> sizes = {n};
-  if (n > 4096) sizes.push_back(4096);
-  if (n > 64) sizes.push_back(64);
+  for (size_t gs : {4096, 256, 16, 2})
+    if (n > gs) sizes.push_back(gs);
   int level = 0;
   for (size_t li = 0; li < sizes.size() && m > 0; li++) {
     const size_t gsize = std::min(sizes[li], m);
@@ -410,13 +411,14 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(w->off.ensure((nk + 1) * 4));
     HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
     HIP_TRY(w->list.ensure(m * g.nwin * 4));
-    HIP_TRY(w->buckets.ensure(nk * jw * 4));
-    HIP_TRY(w->segs.ensure(ngroups * g.nwin * g.nseg * jw * 4));
+    HIP_TRY(w->buckets.ensure(2 * nk * jw * 4));
+    HIP_TRY(w->segs.ensure(2 * ngroups * g.nwin * g.nseg * jw * 4));
     HIP_TRY(w->outA.ensure(ngroups * jw * 4));
     HIP_TRY(w->outB.ensure(ngroups * jw * 4));
+    HIP_TRY(w->out2.ensure(2 * ngroups * jw * 4));
     HIP_TRY(w->pass.ensure(ngroups));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
-                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>()};
+                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>()};
     HIP_TRY(T.run(level == 0 ? "msm_level0" : "msm_bisect", [&] {
       return dh::launch_msm(g2, g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(), w->sig_aff.as<uint32_t>(),
                             w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st);
@@ -706,7 +708,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(w->outA.ensure(jw * 4));
     HIP_TRY(w->outB.ensure((size_t)n_nodes * jw * 4));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
-                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>()};
+                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), nullptr};
     HIP_TRY(T.run("recover_msm_sigs", [&] {
       hipError_t e = dh::launch_msm_sort(gA, w->entries.as<uint32_t>(), nullptr, nullptr, np, 1, w->r_scal.as<uint4>(), ws, st);
       if (e != hipSuccess) return e;
@@ -826,10 +828,11 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(w->off.ensure((nk + 1) * 4));
     HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
     HIP_TRY(w->list.ensure(n_rounds * g.nwin * 4));
-    HIP_TRY(w->buckets.ensure(nk * jw * 4));
-    HIP_TRY(w->segs.ensure((size_t)g.nwin * g.nseg * jw * 4));
+    HIP_TRY(w->buckets.ensure(2 * nk * jw * 4));
+    HIP_TRY(w->segs.ensure(2 * (size_t)g.nwin * g.nseg * jw * 4));
+    HIP_TRY(w->out2.ensure(2 * jw * 4));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
-                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>()};
+                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>()};
     HIP_TRY(T.run("recover_verify", [&] {
       hipError_t e = dh::launch_msm(g2, g, w->r_entries2.as<uint32_t>(), n_rounds, 1, w->r_scal.as<uint4>(),
                                     w->r_aff2.as<uint32_t>(), w->r_q.as<uint32_t>(), ws, w->outA.as<uint32_t>(),

@@ -273,13 +273,30 @@ hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngrou
   return msm_reduce<fp>(g, ngroups, ws.buckets, ws.segs, out, st);
 }
 
+// both point sets of the RLC check in one pass: the buckets of sigma (affine) and of the hash points
+// (Jacobian) sit back to back, so the reduction kernels run once over 2 x ngroups groups (twice the
+// threads in every latency-bound reduction step instead of two serial passes).
 hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
                       const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
                       hipStream_t st) {
   hipError_t e = launch_msm_sort(g, entries, nullptr, nullptr, m, ngroups, scal, ws, st);
   if (e != hipSuccess) return e;
-  if ((e = launch_msm_points(sig_g2, 1, g, ngroups, sig_aff, ws, outA, st)) != hipSuccess) return e;
-  return launch_msm_points(sig_g2, 0, g, ngroups, q_pts, ws, outB, st);
+  const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
+  const size_t jw = sig_g2 ? 72 : 36;
+  uint32_t* bB = ws.buckets + nk * jw;
+  if (sig_g2) {
+    hipLaunchKernelGGL((k_msm_bucket<fp2, true>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, sig_aff, ws.buckets);
+    hipLaunchKernelGGL((k_msm_bucket<fp2, false>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, q_pts, bB);
+    e = msm_reduce<fp2>(g, 2 * ngroups, ws.buckets, ws.segs, ws.out2, st);
+  } else {
+    hipLaunchKernelGGL((k_msm_bucket<fp, true>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, sig_aff, ws.buckets);
+    hipLaunchKernelGGL((k_msm_bucket<fp, false>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, q_pts, bB);
+    e = msm_reduce<fp>(g, 2 * ngroups, ws.buckets, ws.segs, ws.out2, st);
+  }
+  if (e != hipSuccess) return e;
+  const size_t bytes = ngroups * jw * 4;
+  if ((e = hipMemcpyAsync(outA, ws.out2, bytes, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
+  return hipMemcpyAsync(outB, ws.out2 + ngroups * jw, bytes, hipMemcpyDeviceToDevice, st);
 }
 
 hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,

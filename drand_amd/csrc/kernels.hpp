@@ -24,8 +24,9 @@ struct msm_ws {
   uint32_t* off;       // nkeys + 1
   uint32_t* scan_tmp;  // ceil(nkeys / 4096)
   uint32_t* list;      // m * nwin
-  uint32_t* buckets;   // nkeys Jacobian points
-  uint32_t* segs;      // ngroups * nwin * nseg Jacobian points
+  uint32_t* buckets;   // nkeys Jacobian points (x2 for launch_msm: both point sets)
+  uint32_t* segs;      // ngroups * nwin * nseg Jacobian points (x2 for launch_msm)
+  uint32_t* out2;      // launch_msm: 2 * ngroups Jacobian points (sigma sums, then hash sums)
 };
 
 hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n, uint8_t* status, uint32_t* sig_aff,
