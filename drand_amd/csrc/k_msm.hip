@@ -121,7 +121,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
 
 // bucket accumulation: one thread per (group, window, digit) key. P = affine (madd) or Jacobian (add) inputs.
 template <class F, bool AFFINE>
-__global__ __launch_bounds__(256, 4) void k_msm_bucket(const uint32_t* __restrict__ off, const uint32_t* __restrict__ list,
+__global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket(const uint32_t* __restrict__ off, const uint32_t* __restrict__ list,
                                                     size_t nkeys, const uint32_t* __restrict__ pts,
                                                     uint32_t* __restrict__ buckets) {
   size_t k = gtid();
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256, 4) void k_msm_bucket(const uint32_t* __restric
 
 // per (group, window, segment): sum_{d in seg} d * B_d via running sums; seg covers digits [a, a + len)
 template <class F>
-__global__ __launch_bounds__(256, 4) void k_msm_segsum(const uint32_t* __restrict__ buckets, msm_geom g, size_t ngw,
+__global__ __launch_bounds__(256, occ<F>::W) void k_msm_segsum(const uint32_t* __restrict__ buckets, msm_geom g, size_t ngw,
                                                     uint32_t* __restrict__ segs) {
   size_t t = gtid();
   if (t >= ngw * g.nseg) return;
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256, 4) void k_msm_segsum(const uint32_t* __restric
 // pairwise tree reduction in place over rows of `stride` points whose first `width` are live:
 // v[r][c] += v[r][c + half] for c + half < width
 template <class F>
-__global__ __launch_bounds__(256, 4) void k_msm_tree(uint32_t* __restrict__ v, size_t rows, uint32_t stride, uint32_t width,
+__global__ __launch_bounds__(256, occ<F>::W) void k_msm_tree(uint32_t* __restrict__ v, size_t rows, uint32_t stride, uint32_t width,
                                                   uint32_t half) {
   size_t t = gtid();
   if (t >= rows * half) return;

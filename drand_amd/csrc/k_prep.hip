@@ -18,7 +18,7 @@ namespace dh {
 
 // ---------------------------------------------------------------- prep: signatures
 template <class F>
-__global__ __launch_bounds__(256, 4) void k_prep_sig(const uint8_t* __restrict__ sigs, size_t stride, size_t n,
+__global__ __launch_bounds__(256, occ<F>::W) void k_prep_sig(const uint8_t* __restrict__ sigs, size_t stride, size_t n,
                                                   uint8_t* __restrict__ status, uint32_t* __restrict__ sig_aff,
                                                   uint8_t* __restrict__ rand_out) {
   size_t i = gtid();
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256, 4) void k_prep_sig(const uint8_t* __restrict__
 
 // ---------------------------------------------------------------- prep: messages -> hash points (no cofactor)
 template <class F>
-__global__ __launch_bounds__(256, 4) void k_prep_msg(const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs,
+__global__ __launch_bounds__(256, occ<F>::W) void k_prep_msg(const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs,
                                                   size_t prev_stride, const uint32_t* __restrict__ prev_lens, size_t n,
                                                   int chained, int dst_id, uint32_t* __restrict__ q_out) {
   size_t i = gtid();
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256, 4) void k_prep_msg(const uint64_t* __restrict_
 
 // hash points for caller-given 32-byte messages (tbls: the DigestBeacon of each round)
 template <class F>
-__global__ __launch_bounds__(256, 4) void k_prep_msg32(const uint8_t* __restrict__ msgs, size_t n, int dst_id,
+__global__ __launch_bounds__(256, occ<F>::W) void k_prep_msg32(const uint8_t* __restrict__ msgs, size_t n, int dst_id,
                                                        uint32_t* __restrict__ q_out) {
   size_t i = gtid();
   if (i >= n) return;

@@ -6,7 +6,7 @@ namespace dh {
 // ---------------------------------------------------------------- synthetic-chain signer (tests / bench data)
 // sig_i = [sk] H(DigestBeacon(round_i, prev_i)), compressed. Not on the verification path.
 template <class F>
-__global__ __launch_bounds__(256, 4) void k_sign(const uint32_t* __restrict__ sk, const uint64_t* __restrict__ rounds,
+__global__ __launch_bounds__(256, occ<F>::W) void k_sign(const uint32_t* __restrict__ sk, const uint64_t* __restrict__ rounds,
                                                  const uint8_t* __restrict__ prevs, size_t prev_stride,
                                                  const uint32_t* __restrict__ prev_lens, size_t n, int chained, int dst_id,
                                                  uint8_t* __restrict__ out) {

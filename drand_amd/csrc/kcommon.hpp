@@ -90,6 +90,17 @@ struct other<fp2> {
   using T = fp;
 };
 
+// minimum waves per SIMD for the per-round kernels: G1 point code fits 128 VGPRs (4 waves); G2 (Fp2)
+// point code spills heavily at 128, so it gets 256 VGPRs (2 waves) instead
+template <class F>
+struct occ {
+  static constexpr int W = 4;
+};
+template <>
+struct occ<fp2> {
+  static constexpr int W = 2;
+};
+
 DH_DEV size_t gtid() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
 DH_DEV jac<fp> g1_gen() { return {fp_c(cst::G1X), fp_c(cst::G1Y), fp_one()}; }

@@ -192,3 +192,28 @@ def test_recover_threshold_property(dh):
     assert np.array_equal(sigs, want)
     v, _ = s.verify_beacons(commits[0], rounds, sigs, seed=2)
     assert v.all()
+
+
+def test_check_past_beacons_batch_caller(dh):
+    """SyncManager.CheckPastBeacons semantics (chain/beacon/sync_manager.go:170-235) over a trimmed store
+    (chain/boltdb/trimmed.go:156-193); TestDrandCheckChain (core/drand_test.go:1105-1111) expects 2 faulty
+    rounds for a deleted chained beacon and 1 for unchained."""
+    from drand_amd.sync import TrimmedMemStore, check_past_beacons
+    chains = json.load(open(os.path.join(GOLD, "chains.json")))
+    for name, per_delete in (("pedersen-bls-chained", [4, 5]), ("pedersen-bls-unchained", [4])):
+        c = chains[name]
+        s = dh.scheme_from_name(name)
+        st = TrimmedMemStore(s.chained)
+        st.put(0, bytes.fromhex(c["prevs"][0]) if s.chained else b"\x00" * 32)  # genesis
+        for r, sig in zip(c["rounds"], c["sigs"]):
+            st.put(r, bytes.fromhex(sig))
+        pk = bytes.fromhex(c["pk"])
+        seen = []
+        assert check_past_beacons(st, s, pk, 24, cb=lambda i, u: seen.append(i), window=7) == []
+        assert seen == list(range(1, 25))
+        st.delete(4)
+        assert check_past_beacons(st, s, pk, 24, window=5) == per_delete
+        st.put(10, bytes.fromhex(c["sigs"][8]))  # round 10 now stores round 9's signature
+        want = sorted(per_delete + ([10, 11] if s.chained else [10]))
+        assert check_past_beacons(st, s, pk, 24, window=3) == want
+        assert check_past_beacons(st, s, pk, 9) == [x for x in per_delete if x <= 9]
