@@ -67,6 +67,25 @@ DH_DEV fp2 fp2_pow_small(const fp2& x, uint32_t e) {
   return acc;
 }
 
+// x^e for a fixed exponent given as a sliding-window schedule (w = 3, see fp_pow_sched)
+DH_DEV fp2 fp2_pow_sched(const fp2& x, const uint16_t* sched, int len) {
+  const fp2 x2 = fp2_sqr(x);
+  const fp2 t1 = fp2_mul(x, x2);
+  const fp2 t2 = fp2_mul(t1, x2);
+  const fp2 t3 = fp2_mul(t2, x2);
+  auto pick = [&](uint32_t k) { return k == 0 ? x : (k == 1 ? t1 : (k == 2 ? t2 : t3)); };
+  fp2 acc = pick(sched[0]);
+#pragma unroll 1
+  for (int i = 1; i < len; i++) {
+    const uint32_t op = sched[i];
+    const uint32_t nsq = op >> 8, k = op & 0xff;
+#pragma unroll 1
+    for (uint32_t j = 0; j < nsq; j++) acc = fp2_sqr(acc);
+    if (k != 0xff) acc = fp2_mul(acc, pick(k));
+  }
+  return acc;
+}
+
 // RFC 9380 sgn0 for Fp2
 DH_DEV uint32_t fp2_sgn0(const fp2& a) {
   fp c0 = fp_from_mont(a.c0), c1 = fp_from_mont(a.c1);
@@ -82,7 +101,7 @@ DH_DEV bool fp2_sqrt_ratio(fp2& y, const fp2& u, const fp2& v) {
   fp2 tv2 = fp2_pow_small(v, cst::SR2_C4);
   fp2 tv3 = fp2_mul(fp2_sqr(tv2), v);
   fp2 tv5 = fp2_mul(u, tv3);
-  tv5 = fp2_pow_words(tv5, cst::EXP_SR2_C3, cst::EXP_SR2_C3_BITS);
+  tv5 = fp2_pow_sched(tv5, cst::SCHED_SR2_C3, cst::SCHED_SR2_C3_LEN);
   tv5 = fp2_mul(tv5, tv2);
   tv2 = fp2_mul(tv5, v);
   tv3 = fp2_mul(tv5, u);
@@ -108,12 +127,29 @@ DH_DEV bool fp2_sqrt_ratio(fp2& y, const fp2& u, const fp2& v) {
   return isQR;
 }
 
-// square root in Fp2 (any root); false if a is not a square
+// square root in Fp2 (any root); false if a is not a square. "Complex" method for p = 3 mod 4 with three
+// Fp exponentiations and no data-dependent branch:
+//   g = sqrt(a0^2 + a1^2); d = (a0 + g) / 2; s = d^((p+1)/4);
+//   if s^2 == d:  (x0, x1) = (s, a1 / 2s)       else (d is a non-residue, s^2 = -d): (x0, x1) = (a1 / 2s, s)
+// a1 == 0 is handled directly (sqrt(a0) or i sqrt(-a0)). The result is checked by squaring.
 DH_DEV bool fp2_sqrt(fp2& r, const fp2& a) {
-  fp2 y;
-  bool qr = fp2_sqrt_ratio(y, a, fp2_one());
-  r = y;
-  return qr && fp2_eq(fp2_sqr(y), a);
+  if (fp_is_zero(a.c1)) {
+    fp s0, s1;
+    bool q0 = fp_sqrt(s0, a.c0);
+    bool q1 = fp_sqrt(s1, fp_neg(a.c0));
+    r = q0 ? fp2{s0, fp_zero()} : fp2{fp_zero(), s1};
+    return q0 || q1;
+  }
+  fp g;
+  fp_sqrt(g, fp_add(fp_sqr(a.c0), fp_sqr(a.c1)));  // a non-square norm shows up in the final check
+  fp d = fp_add(a.c0, g);
+  d = fp_is_zero(d) ? fp_sub(a.c0, g) : d;
+  d = fp_mul(d, fp_c(cst::INV2));
+  fp s;
+  bool qr = fp_sqrt(s, d);
+  fp t = fp_mul(a.c1, fp_inv(fp_dbl(s)));  // a1 / 2s
+  r = qr ? fp2{s, t} : fp2{t, s};
+  return fp2_eq(fp2_sqr(r), a);
 }
 
 }  // namespace dh

@@ -320,6 +320,7 @@ def main():
     fp2_const("SSWU2_Z", Z2)
     fp2_const("SQRT_RATIO2_C6", c6)
     fp2_const("SQRT_RATIO2_C7", c7)
+    fp_const("INV2", (P + 1) // 2)  # 1/2
     fp_const("K256", k256)
     fp_const("K256R", k256 * MONT % P)  # mont_mul(raw hi, K256R) = Mont(hi * 2^256)
     fp_const("R2", MONT % P)  # c_fp(R) = R^2 mod p: mont_mul(raw x, R2) = Mont(x)
@@ -342,7 +343,7 @@ def main():
     # sliding-window (w = 3, odd powers x^1,3,5,7) schedules for the fixed Fp exponents:
     # entry = (squarings << 8) | table index, index 0xff = squarings only (trailing zeros)
     for name, e in (("SCHED_SQRT", (P + 1) // 4), ("SCHED_SR1_C1", sr1_c1), ("SCHED_INV", P - 2),
-                    ("SCHED_LEGENDRE", (P - 1) // 2)):
+                    ("SCHED_LEGENDRE", (P - 1) // 2), ("SCHED_SR2_C3", c3)):
         sched = window_schedule(e, 3)
         w("constexpr int %s_LEN = %d;" % (name, len(sched)))
         w("__device__ __constant__ uint16_t %s[%d] = {%s};" % (name, len(sched), ", ".join("0x%04x" % v for v in sched)))
