@@ -94,7 +94,7 @@ struct other<fp2> {
 // point code spills heavily at 128, so it gets 256 VGPRs (2 waves) instead
 template <class F>
 struct occ {
-  static constexpr int W = 4;
+  static constexpr int W = 2;
 };
 template <>
 struct occ<fp2> {
