@@ -20,6 +20,31 @@ __global__ void k_fips(dh::fp* out, const dh::fp* in) {
   for (int it = 0; it < IT; it++) { dh::fips_mont_mul(x.v, x.v, y.v); dh::fips_mont_mul(z.v, z.v, y.v); }
   out[gid] = dh::fp_add(x, z);
 }
+__global__ void k_fips1(dh::fp* out, const dh::fp* in) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  dh::fp x = in[gid & 1023], y = in[(gid + 1) & 1023], z = in[(gid + 2) & 1023];
+  for (int it = 0; it < IT; it++) { dh::fips_mont_mul1(x.v, x.v, y.v); dh::fips_mont_mul1(z.v, z.v, y.v); }
+  out[gid] = dh::fp_add(x, z);
+}
+__global__ void k_fsqr1(dh::fp* out, const dh::fp* in) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  dh::fp x = in[gid & 1023], z = in[(gid + 2) & 1023];
+  for (int it = 0; it < IT; it++) { dh::fips_mont_sqr1(x.v, x.v); dh::fips_mont_sqr1(z.v, z.v); }
+  out[gid] = dh::fp_add(x, z);
+}
+// the production form: out-of-line vector-ABI calls (fp.hpp fp_mul / fp_sqr)
+__global__ void k_call_mul(dh::fp* out, const dh::fp* in) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  dh::fp x = in[gid & 1023], y = in[(gid + 1) & 1023], z = in[(gid + 2) & 1023];
+  for (int it = 0; it < IT; it++) { x = dh::fp_mul(x, y); z = dh::fp_mul(z, y); }
+  out[gid] = dh::fp_add(x, z);
+}
+__global__ void k_call_sqr(dh::fp* out, const dh::fp* in) {
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  dh::fp x = in[gid & 1023], z = in[(gid + 2) & 1023];
+  for (int it = 0; it < IT; it++) { x = dh::fp_sqr(x); z = dh::fp_sqr(z); }
+  out[gid] = dh::fp_add(x, z);
+}
 __global__ void k_fipsc(dh::fp* out, const dh::fp* in) {
   int gid = blockIdx.x * blockDim.x + threadIdx.x;
   dh::fp x = in[gid & 1023], y = in[(gid + 1) & 1023], z = in[(gid + 2) & 1023];
@@ -61,13 +86,23 @@ static void host_mont(uint32_t* r32, const uint32_t* a32, const uint32_t* b32) {
   memcpy(r32, t, 48);
 }
 
+// occupancy-limited variant: dynamic LDS caps resident 256-thread blocks per CU (1 block = 1 wave/SIMD)
+extern "C" __global__ void k_call_mul_lds(dh::fp* out, const dh::fp* in) {
+  extern __shared__ uint32_t pad[];
+  int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  dh::fp x = in[gid & 1023], y = in[(gid + 1) & 1023], z = in[(gid + 2) & 1023];
+  for (int it = 0; it < IT; it++) { x = dh::fp_mul(x, y); z = dh::fp_mul(z, y); }
+  if (gid < 0) pad[threadIdx.x] = 0;
+  out[gid] = dh::fp_add(x, z);
+}
+
 template <typename K>
-float tk(K k, int blocks, dh::fp* o, const dh::fp* i) {
+float tk(K k, int blocks, dh::fp* o, const dh::fp* i, size_t lds = 0) {
   hipEvent_t s, e; hipEventCreate(&s); hipEventCreate(&e);
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, o, i);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, o, i);
   hipDeviceSynchronize();
   hipEventRecord(s);
-  for (int r = 0; r < 5; r++) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, o, i);
+  for (int r = 0; r < 5; r++) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, 0, o, i);
   hipEventRecord(e); hipEventSynchronize(e);
   float ms; hipEventElapsedTime(&ms, s, e);
   return ms / 5;
@@ -113,6 +148,18 @@ int main() {
       if (memcmp(t, r3[g].v, 48)) bad |= 8;
     }
     for (int g = 0; g < 1024; g++) if (memcmp(r1[1024 + g].v, r2[1024 + g].v, 48)) bad |= 4;
+    // old single-MAC forms and the out-of-line call forms agree with the grouped ones
+    static dh::fp q1[1024], q2[1024];
+    hipLaunchKernelGGL(k_fips1, dim3(4), dim3(256), 0, 0, o2, in);
+    hipMemcpy(q1, o2, sizeof(q1), hipMemcpyDeviceToHost);
+    hipLaunchKernelGGL(k_call_mul, dim3(4), dim3(256), 0, 0, o2, in);
+    hipMemcpy(q2, o2, sizeof(q2), hipMemcpyDeviceToHost);
+    for (int g = 0; g < 1024; g++) if (memcmp(q1[g].v, r1[g].v, 48) || memcmp(q2[g].v, r1[g].v, 48)) bad |= 16;
+    hipLaunchKernelGGL(k_fsqr1, dim3(4), dim3(256), 0, 0, o2, in);
+    hipMemcpy(q1, o2, sizeof(q1), hipMemcpyDeviceToHost);
+    hipLaunchKernelGGL(k_call_sqr, dim3(4), dim3(256), 0, 0, o2, in);
+    hipMemcpy(q2, o2, sizeof(q2), hipMemcpyDeviceToHost);
+    for (int g = 0; g < 1024; g++) if (memcmp(q1[g].v, r1[1024 + g].v, 48) || memcmp(q2[g].v, r1[1024 + g].v, 48)) bad |= 32;
   }
   printf("{\"check\": \"fp_mul fips/cios/sqr vs host\", \"bad_mask\": %d}\n", bad);
   double ops = (double)n * IT * 2;
@@ -120,6 +167,20 @@ int main() {
   printf("{\"op\": \"fp_mul_cios\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
   ms = tk(k_fips, blocks, o1, in);
   printf("{\"op\": \"fp_mul_fips\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
+  ms = tk(k_fips1, blocks, o1, in);
+  printf("{\"op\": \"fp_mul_fips_1mac_per_asm\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
+  ms = tk(k_fsqr1, blocks, o1, in);
+  printf("{\"op\": \"fp_sqr_fips_1mac_per_asm\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
+  ms = tk(k_call_mul, blocks, o1, in);
+  printf("{\"op\": \"fp_mul_call (production)\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
+  ms = tk(k_call_sqr, blocks, o1, in);
+  printf("{\"op\": \"fp_sqr_call (production)\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
+  hipFuncSetAttribute((const void*)k_call_mul_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (int w : {1, 2, 3, 4}) {
+    size_t lds = (160 * 1024) / w - 1024;
+    ms = tk(k_call_mul_lds, blocks, o1, in, lds);
+    printf("{\"op\": \"fp_mul_call, occupancy %d wave/SIMD\", \"Gops_per_s\": %.2f}\n", w, ops / ms / 1e6);
+  }
   ms = tk(k_fipsc, blocks, o1, in);
   printf("{\"op\": \"fp_mul_fips_plain_c\", \"Gops_per_s\": %.2f}\n", ops / ms / 1e6);
   ms = tk(k_csqr, blocks, o1, in);

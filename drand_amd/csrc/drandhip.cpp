@@ -86,7 +86,7 @@ struct worker {
   // key
   dbuf key_raw, key_aff, key_ok;
   // MSM
-  dbuf cnt, off, scan_tmp, list, buckets, segs, outA, outB, out2, pass;
+  dbuf cnt, off, scan_tmp, list, buckets, segs, outA, outB, out2, pass, part, meta;
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
@@ -101,7 +101,7 @@ struct worker {
   void release_all() {
     dbuf* all[] = {&status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
-                   &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &r_commits, &r_cstatus, &r_caff, &r_shares,
+                   &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
                    &r_sigbytes, &r_status2, &r_aff2, &r_entries2};
@@ -417,8 +417,11 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(w->outB.ensure(ngroups * jw * 4));
     HIP_TRY(w->out2.ensure(2 * ngroups * jw * 4));
     HIP_TRY(w->pass.ensure(ngroups));
+    HIP_TRY(w->part.ensure(dh::msm_part_bytes(m * g.nwin, jw, 2)));
+    HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(m * g.nwin)));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
-                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>()};
+                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>(), w->part.as<uint32_t>(),
+                  w->meta.as<uint32_t>(), 0};
     HIP_TRY(T.run(level == 0 ? "msm_level0" : "msm_bisect", [&] {
       return dh::launch_msm(g2, g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(), w->sig_aff.as<uint32_t>(),
                             w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st);
@@ -707,8 +710,12 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(w->segs.ensure(std::max((size_t)gA.nwin * gA.nseg, (size_t)n_nodes * gB.nwin * gB.nseg) * jw * 4));
     HIP_TRY(w->outA.ensure(jw * 4));
     HIP_TRY(w->outB.ensure((size_t)n_nodes * jw * 4));
+    const size_t max_ent = std::max(np * gA.nwin, mB * gB.nwin);
+    HIP_TRY(w->part.ensure(dh::msm_part_bytes(max_ent, jw, 1)));
+    HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(max_ent)));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
-                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), nullptr};
+                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), nullptr, w->part.as<uint32_t>(),
+                  w->meta.as<uint32_t>(), 0};
     HIP_TRY(T.run("recover_msm_sigs", [&] {
       hipError_t e = dh::launch_msm_sort(gA, w->entries.as<uint32_t>(), nullptr, nullptr, np, 1, w->r_scal.as<uint4>(), ws, st);
       if (e != hipSuccess) return e;
@@ -831,8 +838,11 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(w->buckets.ensure(2 * nk * jw * 4));
     HIP_TRY(w->segs.ensure(2 * (size_t)g.nwin * g.nseg * jw * 4));
     HIP_TRY(w->out2.ensure(2 * jw * 4));
+    HIP_TRY(w->part.ensure(dh::msm_part_bytes(n_rounds * g.nwin, jw, 2)));
+    HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(n_rounds * g.nwin)));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
-                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>()};
+                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>(), w->part.as<uint32_t>(),
+                  w->meta.as<uint32_t>(), 0};
     HIP_TRY(T.run("recover_verify", [&] {
       hipError_t e = dh::launch_msm(g2, g, w->r_entries2.as<uint32_t>(), n_rounds, 1, w->r_scal.as<uint4>(),
                                     w->r_aff2.as<uint32_t>(), w->r_q.as<uint32_t>(), ws, w->outA.as<uint32_t>(),

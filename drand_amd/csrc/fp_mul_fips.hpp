@@ -10,6 +10,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
+#include "fp_mac_n.hpp"
+
 namespace dh {
 
 // acc(64) += x*y, carry into hi32. The carry-out lane mask goes through an SGPR pair the compiler
@@ -24,7 +28,7 @@ namespace dh {
                  : "v"(x), "v"(y));                                                                 \
   } while (0)
 
-__device__ __forceinline__ void fips_mont_mul(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
+__device__ __forceinline__ void fips_mont_mul1(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
   constexpr uint32_t P[12] = {0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u,
                               0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau};
   constexpr uint32_t NP0 = 0xfffcfffdu;
@@ -67,7 +71,7 @@ __device__ __forceinline__ void fips_mont_mul(uint32_t r[12], const uint32_t a[1
 }
 
 // squaring: off-diagonal products once, doubled, plus the diagonal (222 instead of 288 partial products)
-__device__ __forceinline__ void fips_mont_sqr(uint32_t r[12], const uint32_t a[12]) {
+__device__ __forceinline__ void fips_mont_sqr1(uint32_t r[12], const uint32_t a[12]) {
   constexpr uint32_t P[12] = {0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u,
                               0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau};
   constexpr uint32_t NP0 = 0xfffcfffdu;
@@ -123,6 +127,131 @@ __device__ __forceinline__ void fips_mont_sqr(uint32_t r[12], const uint32_t a[1
 #pragma unroll
   for (int i = 0; i < 12; i++) r[i] = br ? r[i] : d[i];
 }
+
+// Column-statement form (the one used): every column's partial products are ONE inline-asm statement
+// (fp_mac_n.hpp, generated). The hazard recognizer assumes a one-wait-state dst-forwarding hazard between
+// two inline-asm statements that share a register (gfx940+), so one MAC per statement costs an s_nop 0 per
+// partial product (252 of them in fips_mont_mul1); one statement per column leaves ~1 per column. Inside a
+// statement, v_mad_u64_u32 (carry-out to an SGPR pair) followed by v_addc_co_u32 reading it is the
+// ordinary VALU-writes-SGPR / VALU-reads-carry sequence of the compiler's own 64-bit adds.
+#define DH_P_LIMBS                                                                                      \
+  {0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u,                        \
+   0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau}
+
+template <int K>
+__device__ __forceinline__ void mul_col(uint64_t& acc, uint32_t& hi, uint32_t m[12], uint32_t r[12],
+                                        const uint32_t a[12], const uint32_t b[12], const uint32_t P[12]) {
+  constexpr uint32_t NP0 = 0xfffcfffdu;
+  constexpr int LO = K > 11 ? K - 11 : 0, UP = K < 12 ? K : 11, MUP = K < 12 ? K - 1 : 11;
+  constexpr int C = (UP - LO + 1) + (MUP >= LO ? MUP - LO + 1 : 0);
+  uint32_t xs[C], ys[C];
+  int c = 0;
+#pragma unroll
+  for (int i = LO; i <= UP; i++) { xs[c] = a[i]; ys[c] = b[K - i]; c++; }
+#pragma unroll
+  for (int i = LO; i <= MUP; i++) { xs[c] = m[i]; ys[c] = P[K - i]; c++; }
+  mac_n<C>(acc, hi, xs, ys);
+  if constexpr (K < 12) {
+    m[K] = (uint32_t)acc * NP0;
+    uint32_t p0 = P[0];
+    mac_n<1>(acc, hi, &m[K], &p0);  // low word becomes 0
+  } else {
+    r[K - 12] = (uint32_t)acc;
+  }
+  acc = (acc >> 32) | ((uint64_t)hi << 32);
+  hi = 0;
+}
+
+template <int K>
+__device__ __forceinline__ void sqr_col(uint64_t& acc, uint32_t& hi, uint32_t m[12], uint32_t r[12],
+                                        const uint32_t a[12], const uint32_t P[12]) {
+  constexpr uint32_t NP0 = 0xfffcfffdu;
+  constexpr int LO = K > 11 ? K - 11 : 0, MUP = K < 12 ? K - 1 : 11;
+  constexpr int D = (K + 1) / 2 - LO > 0 ? (K + 1) / 2 - LO : 0;  // pairs i < K-i, i >= LO
+  constexpr int CM = MUP >= LO ? MUP - LO + 1 : 0;
+  uint64_t s = 0;
+  uint32_t sh = 0;
+  if constexpr (D > 0) {
+    uint32_t xs[D], ys[D];
+#pragma unroll
+    for (int j = 0; j < D; j++) { xs[j] = a[LO + j]; ys[j] = a[K - LO - j]; }
+    mac_n<D>(s, sh, xs, ys);
+    sh = (sh << 1) | (uint32_t)(s >> 63);
+    s <<= 1;
+  }
+  if constexpr ((K & 1) == 0) mac_n<1>(s, sh, &a[K >> 1], &a[K >> 1]);
+  {
+    uint32_t slo = (uint32_t)s, shi = (uint32_t)(s >> 32);
+    uint32_t alo = (uint32_t)acc, ahi = (uint32_t)(acc >> 32);
+    uint64_t c_;
+    asm volatile(
+        "v_add_co_u32_e64 %0, %3, %0, %4\n\t"
+        "v_addc_co_u32_e64 %1, %3, %1, %5, %3\n\t"
+        "v_addc_co_u32_e64 %2, %3, %2, %6, %3"
+        : "+v"(alo), "+v"(ahi), "+v"(hi), "=&s"(c_)
+        : "v"(slo), "v"(shi), "v"(sh));
+    acc = (uint64_t)alo | ((uint64_t)ahi << 32);
+  }
+  if constexpr (CM > 0) {
+    uint32_t xs[CM], ys[CM];
+#pragma unroll
+    for (int j = 0; j < CM; j++) { xs[j] = m[LO + j]; ys[j] = P[K - LO - j]; }
+    mac_n<CM>(acc, hi, xs, ys);
+  }
+  if constexpr (K < 12) {
+    m[K] = (uint32_t)acc * NP0;
+    uint32_t p0 = P[0];
+    mac_n<1>(acc, hi, &m[K], &p0);
+  } else {
+    r[K - 12] = (uint32_t)acc;
+  }
+  acc = (acc >> 32) | ((uint64_t)hi << 32);
+  hi = 0;
+}
+
+template <int... K>
+__device__ __forceinline__ void mul_cols(std::integer_sequence<int, K...>, uint64_t& acc, uint32_t& hi, uint32_t m[12],
+                                         uint32_t r[12], const uint32_t a[12], const uint32_t b[12], const uint32_t P[12]) {
+  (mul_col<K>(acc, hi, m, r, a, b, P), ...);
+}
+template <int... K>
+__device__ __forceinline__ void sqr_cols(std::integer_sequence<int, K...>, uint64_t& acc, uint32_t& hi, uint32_t m[12],
+                                         uint32_t r[12], const uint32_t a[12], const uint32_t P[12]) {
+  (sqr_col<K>(acc, hi, m, r, a, P), ...);
+}
+
+__device__ __forceinline__ void fips_final_sub(uint32_t r[12], uint64_t acc, const uint32_t P[12]) {
+  r[11] = (uint32_t)acc;  // < 2p < 2^382: no further carry
+  uint32_t d[12];
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    uint64_t t = (uint64_t)r[i] - P[i] - br;
+    d[i] = (uint32_t)t;
+    br = (t >> 63) & 1;
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) r[i] = br ? r[i] : d[i];
+}
+
+__device__ __forceinline__ void fips_mont_mul(uint32_t r[12], const uint32_t a[12], const uint32_t b[12]) {
+  const uint32_t P[12] = DH_P_LIMBS;
+  uint32_t m[12];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+  mul_cols(std::make_integer_sequence<int, 23>{}, acc, hi, m, r, a, b, P);
+  fips_final_sub(r, acc, P);
+}
+
+__device__ __forceinline__ void fips_mont_sqr(uint32_t r[12], const uint32_t a[12]) {
+  const uint32_t P[12] = DH_P_LIMBS;
+  uint32_t m[12];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+  sqr_cols(std::make_integer_sequence<int, 23>{}, acc, hi, m, r, a, P);
+  fips_final_sub(r, acc, P);
+}
+#undef DH_P_LIMBS
 
 #undef DH_MAC
 

@@ -119,24 +119,105 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
   }
 }
 
-// bucket accumulation: one thread per (group, window, digit) key. P = affine (madd) or Jacobian (add) inputs.
+// Bucket accumulation, load-balanced: the sorted list (bucket by bucket, all keys back to back) is cut
+// into chunks of L consecutive entries, one thread per chunk, so every lane does the same number of point
+// additions whatever the bucket sizes (one thread per bucket left the wave waiting for its fullest
+// bucket: Poisson(16) sizes at c = 16). A key that lies wholly inside a chunk is written to its bucket
+// directly; a key cut by chunk boundaries leaves partial sums: the chunk where it starts keeps a "tail"
+// partial, each later chunk it covers a "head" partial (kind 1: the key ends in that chunk, kind 2: it
+// covers the whole chunk), and k_msm_bucket_fix adds them up. Buckets of empty keys stay at the zeroed
+// (Z = 0, infinity) value the launcher writes first.
+constexpr uint32_t NO_KEY = 0xffffffffu;
+
 template <class F, bool AFFINE>
 __global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket(const uint32_t* __restrict__ off, const uint32_t* __restrict__ list,
-                                                    size_t nkeys, const uint32_t* __restrict__ pts,
-                                                    uint32_t* __restrict__ buckets) {
-  size_t k = gtid();
-  if (k >= nkeys) return;
-  uint32_t b = off[k], e = off[k + 1];
+                                                    size_t nkeys, uint32_t L, const uint32_t* __restrict__ pts,
+                                                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ part,
+                                                    uint32_t* __restrict__ meta) {
+  const size_t t = gtid();
+  const uint32_t total = off[nkeys];
+  const size_t s = t * (size_t)L;
+  if (s >= total) return;
+  const uint32_t e = (uint32_t)min(s + L, (size_t)total);
+  // the key holding entry s: the largest k with off[k] <= s (off[nkeys] = total > s)
+  size_t lo = 0, hi = nkeys;
+  while (hi - lo > 1) {
+    size_t mid = (lo + hi) >> 1;
+    if (off[mid] <= s) lo = mid;
+    else hi = mid;
+  }
+  size_t key = lo;
+  uint32_t kend = off[key + 1];
+  const bool starts_before = off[key] < s;
+  bool first = true;
+  uint32_t head_kind = 0, tail_key = NO_KEY;
   jac<F> acc = jac_inf<F>();
-  for (uint32_t j = b; j < e; j++) {
-    uint32_t idx = list[j];
+  for (uint32_t j = (uint32_t)s; j < e; j++) {
+    const uint32_t idx = list[j];
     if constexpr (AFFINE) {
       acc = jac_add_aff(acc, ld_aff_aos<F>(pts, idx));
     } else {
       acc = jac_add(acc, ld_jac_aos<F>(pts, idx));
     }
+    const bool ends = j + 1 == kend;
+    if (ends || j + 1 == e) {
+      if (first && starts_before) {
+        st_jac_aos<F>(part, 2 * t, acc);
+        head_kind = ends ? 1 : 2;
+      } else if (ends) {
+        st_jac_aos<F>(buckets, key, acc);
+      } else {
+        st_jac_aos<F>(part, 2 * t + 1, acc);
+        tail_key = (uint32_t)key;
+      }
+      first = false;
+      if (ends && j + 1 < e) {  // next non-empty key starts at entry j + 1
+        do {
+          key++;
+        } while (off[key + 1] <= j + 1);
+        kend = off[key + 1];
+        acc = jac_inf<F>();
+      }
+    }
   }
-  st_jac_aos<F>(buckets, k, acc);
+  if (meta) {
+    meta[2 * t] = head_kind;
+    meta[2 * t + 1] = tail_key;
+  }
+}
+
+// one thread per chunk that holds a tail partial: add the head partials of the following chunks the key covers
+template <class F>
+__global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket_fix(const uint32_t* __restrict__ off, size_t nkeys, uint32_t L,
+                                                        const uint32_t* __restrict__ meta, const uint32_t* __restrict__ part,
+                                                        uint32_t* __restrict__ buckets) {
+  const size_t t = gtid();
+  const uint32_t total = off[nkeys];
+  const size_t nch = (total + L - 1) / L;
+  if (t >= nch) return;
+  const uint32_t key = meta[2 * t + 1];
+  if (key == NO_KEY) return;
+  jac<F> acc = ld_jac_aos<F>(part, 2 * t + 1);
+  for (size_t u = t + 1; u < nch; u++) {
+    acc = jac_add(acc, ld_jac_aos<F>(part, 2 * u));
+    if (meta[2 * u] == 1) break;
+  }
+  st_jac_aos<F>(buckets, key, acc);
+}
+
+template <class F, bool AFFINE>
+static hipError_t launch_buckets(const msm_ws& ws, size_t nk, const uint32_t* pts, uint32_t* buckets, uint32_t* part,
+                                 bool write_meta, hipStream_t st) {
+  constexpr size_t jw = sizeof(F) / 4 * 3;
+  hipError_t e = hipMemsetAsync(buckets, 0, nk * jw * 4, st);
+  if (e != hipSuccess) return e;
+  if (!ws.max_entries) return hipSuccess;
+  const uint32_t L = msm_chunk_len(ws.max_entries);
+  const size_t nch = (ws.max_entries + L - 1) / L;
+  hipLaunchKernelGGL((k_msm_bucket<F, AFFINE>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, pts, buckets,
+                     part, write_meta ? ws.meta : nullptr);
+  hipLaunchKernelGGL((k_msm_bucket_fix<F>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, nk, L, ws.meta, part, buckets);
+  return hipGetLastError();
 }
 
 // per (group, window, segment): sum_{d in seg} d * B_d via running sums; seg covers digits [a, a + len)
@@ -246,6 +327,7 @@ static hipError_t msm_reduce(const msm_geom& g, size_t ngroups, uint32_t* bucket
 hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp, size_t m,
                            size_t ngroups, const uint4* scal, msm_ws& ws, hipStream_t st) {
   size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
+  ws.max_entries = m * (size_t)g.nwin;
   hipError_t e = hipMemsetAsync(ws.cnt, 0, nk * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   if (m) hipLaunchKernelGGL(k_msm_hist, dim3(nblk(m, 256)), dim3(256), 0, st, pidx, sidx, grp, m, scal, g, ws.cnt);
@@ -259,17 +341,16 @@ hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32
 hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngroups, const uint32_t* pts, msm_ws& ws,
                              uint32_t* out, hipStream_t st) {
   size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
+  hipError_t e;
   if (g2) {
-    if (affine)
-      hipLaunchKernelGGL((k_msm_bucket<fp2, true>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, pts, ws.buckets);
-    else
-      hipLaunchKernelGGL((k_msm_bucket<fp2, false>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, pts, ws.buckets);
+    e = affine ? launch_buckets<fp2, true>(ws, nk, pts, ws.buckets, ws.part, true, st)
+               : launch_buckets<fp2, false>(ws, nk, pts, ws.buckets, ws.part, true, st);
+    if (e != hipSuccess) return e;
     return msm_reduce<fp2>(g, ngroups, ws.buckets, ws.segs, out, st);
   }
-  if (affine)
-    hipLaunchKernelGGL((k_msm_bucket<fp, true>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, pts, ws.buckets);
-  else
-    hipLaunchKernelGGL((k_msm_bucket<fp, false>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, pts, ws.buckets);
+  e = affine ? launch_buckets<fp, true>(ws, nk, pts, ws.buckets, ws.part, true, st)
+             : launch_buckets<fp, false>(ws, nk, pts, ws.buckets, ws.part, true, st);
+  if (e != hipSuccess) return e;
   return msm_reduce<fp>(g, ngroups, ws.buckets, ws.segs, out, st);
 }
 
@@ -284,13 +365,15 @@ hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, si
   const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
   const size_t jw = sig_g2 ? 72 : 36;
   uint32_t* bB = ws.buckets + nk * jw;
+  // the partial sums of the two point sets sit back to back; the chunk metadata is the same for both
+  uint32_t* pB = ws.part + msm_nchunks(ws.max_entries) * 2 * jw;
   if (sig_g2) {
-    hipLaunchKernelGGL((k_msm_bucket<fp2, true>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, sig_aff, ws.buckets);
-    hipLaunchKernelGGL((k_msm_bucket<fp2, false>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, q_pts, bB);
+    if ((e = launch_buckets<fp2, true>(ws, nk, sig_aff, ws.buckets, ws.part, true, st)) != hipSuccess) return e;
+    if ((e = launch_buckets<fp2, false>(ws, nk, q_pts, bB, pB, false, st)) != hipSuccess) return e;
     e = msm_reduce<fp2>(g, 2 * ngroups, ws.buckets, ws.segs, ws.out2, st);
   } else {
-    hipLaunchKernelGGL((k_msm_bucket<fp, true>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, sig_aff, ws.buckets);
-    hipLaunchKernelGGL((k_msm_bucket<fp, false>), dim3(nblk(nk, 256)), dim3(256), 0, st, ws.off, ws.list, nk, q_pts, bB);
+    if ((e = launch_buckets<fp, true>(ws, nk, sig_aff, ws.buckets, ws.part, true, st)) != hipSuccess) return e;
+    if ((e = launch_buckets<fp, false>(ws, nk, q_pts, bB, pB, false, st)) != hipSuccess) return e;
     e = msm_reduce<fp>(g, 2 * ngroups, ws.buckets, ws.segs, ws.out2, st);
   }
   if (e != hipSuccess) return e;

@@ -27,7 +27,21 @@ struct msm_ws {
   uint32_t* buckets;   // nkeys Jacobian points (x2 for launch_msm: both point sets)
   uint32_t* segs;      // ngroups * nwin * nseg Jacobian points (x2 for launch_msm)
   uint32_t* out2;      // launch_msm: 2 * ngroups Jacobian points (sigma sums, then hash sums)
+  uint32_t* part;      // balanced bucket pass: 2 Jacobian partial sums per chunk (x2 for launch_msm)
+  uint32_t* meta;      // balanced bucket pass: 2 words per chunk (head kind, tail key)
+  size_t max_entries;  // set by launch_msm_sort: upper bound of sorted-list entries (m * nwin)
 };
+
+// balanced bucket accumulation: entries per chunk, and workspace sizes for `max_entries` list entries
+inline uint32_t msm_chunk_len(size_t max_entries) {
+  size_t L = max_entries / 262144;
+  return (uint32_t)(L < 4 ? 4 : L > 32 ? 32 : L);
+}
+inline size_t msm_nchunks(size_t max_entries) { return max_entries / msm_chunk_len(max_entries) + 2; }
+inline size_t msm_part_bytes(size_t max_entries, size_t jac_words, int nsets) {
+  return msm_nchunks(max_entries) * 2 * jac_words * 4 * (size_t)nsets;
+}
+inline size_t msm_meta_bytes(size_t max_entries) { return msm_nchunks(max_entries) * 2 * 4; }
 
 hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n, uint8_t* status, uint32_t* sig_aff,
                        uint8_t* rand_out, hipStream_t st);
