@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--roofline-steps", type=int, default=2, help="single-stream batches timed for the roofline")
     ap.add_argument("--streams", type=int, default=3,
                     help="batches in flight per GPU (host threads, each with its own HIP stream in libdrandhip)")
     return ap.parse_args()
@@ -116,8 +117,8 @@ def main():
         if rc != 0:
             raise RuntimeError("dh_verify_batch_device: %s" % _lib.last_error())
 
-    def run_steps(k_steps):
-        """k_steps batches, S in flight: thread t runs steps t, t+S, ... on its own output slot."""
+    def run_steps(k_steps, streams):
+        """k_steps batches, `streams` in flight: thread t runs steps t, t+streams, ... on its own output slot."""
         import threading
         errs = []
         bits = [None] * k_steps
@@ -125,13 +126,13 @@ def main():
         def worker(t):
             try:
                 torch.cuda.set_device(local)
-                for k in range(t, k_steps, S):
+                for k in range(t, k_steps, streams):
                     verify(t)
                     bits[k] = pack_bits(d_verdict[t])
             except Exception as e:  # surfaced below
                 errs.append(e)
 
-        ths = [threading.Thread(target=worker, args=(t,)) for t in range(min(S, k_steps))]
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(min(streams, k_steps))]
         for th in ths:
             th.start()
         for th in ths:
@@ -142,21 +143,32 @@ def main():
             gather_verdicts(torch.cat(bits), world)
         torch.cuda.synchronize()
 
-    run_steps(max(args.warmup, 1) if args.warmup else 0)
+    def profile_read():
+        buf = ctypes.create_string_buffer(1 << 16)
+        lib.dh_profile_read(buf, len(buf))
+        return json.loads(buf.value.decode())
+
+    run_steps(max(args.warmup, 1) if args.warmup else 0, S)
     lib.dh_profile(1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_steps(args.steps)
+    run_steps(args.steps, S)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    buf = ctypes.create_string_buffer(1 << 16)
-    lib.dh_profile_read(buf, len(buf))
+    prof = profile_read()
+    # Roofline pass (after the timed region, not counted in `value`): with S batches in flight the kernels of
+    # different batches share the CUs, so per-launch durations measured there are not one kernel's speed.
+    # Two more batches on ONE stream give each kernel the whole GPU; the dominant kernel's roofline is
+    # computed from their HIP events (recorded on the library's stream). bench/profile.sh collects the
+    # rocprofv3 kernel-trace of the same single-stream batches.
+    lib.dh_profile(1)
+    run_steps(args.roofline_steps, 1)
+    prof1 = profile_read()
     lib.dh_profile(0)
-    prof = json.loads(buf.value.decode())
 
     # sanity (outside the timed region): every synthetic round verifies, randomness = SHA-256(sig)
     ok = all(bool(d.cpu().numpy().all()) for d in d_verdict[:min(S, args.steps)])
@@ -176,20 +188,25 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     value = world * n * args.steps / elapsed
     peak = wm["peak_mul32_per_s_measured"]
-    kern = {k: v for k, v in prof.items() if k.startswith("k_prep")}
+    kern = {k: v for k, v in prof1.items() if k.startswith("k_prep")}
     dom = max(kern, key=lambda k: kern[k]["total_ms"]) if kern else None
     roof = None
     if dom:
         avg_s = kern[dom]["total_ms"] / kern[dom]["count"] / 1000.0
         units = wm["kernel_units_M_per_round"][dom] * wm["mul32_per_M"] * n
         achieved = units / avg_s / 1e12
-        traffic = None
+        traffic = None  # HBM bytes per launch from the committed PMC passes (bench/profile.sh, pmc_summary.py)
         pmc = os.path.join(ROOT, "profiles", "pmc_r01.json")
         if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+            per_round = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_round")
+            traffic = round(per_round * n) if per_round is not None else None
         roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak / 1e12, 3),
                 "unit": "Tmul32/s", "frac": round(achieved * 1e12 / peak, 4), "traffic": traffic,
-                "avg_launch_ms": round(avg_s * 1000, 3)}
+                "traffic_unit": "bytes per launch (FETCH+WRITE, PMC)",
+                "avg_launch_ms": round(avg_s * 1000, 3),
+                "work_per_launch": "%d M x %d mul32 x %d rounds" % (wm["kernel_units_M_per_round"][dom],
+                                                                   wm["mul32_per_M"], n),
+                "measured": "HIP events, %d single-stream batches after the timed region" % args.roofline_steps}
     w_beacon = wm["W_M_per_beacon"]["g2_sig" if sch.sig_len == 96 else "g1_sig"] * wm["mul32_per_M"]
     out = {
         "metric": "verified beacons/sec (whole node), quicknet G1 scheme" if sch.id == 3 else
@@ -204,6 +221,7 @@ def main():
         "verdicts_ok": ok,
         "streams": S,
         "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in prof.items()},
+        "stages_ms_single_stream": {k: round(v["total_ms"] / max(1, v["count"]), 3) for k, v in prof1.items()},
         "sign_seconds": round(t_sign, 2),
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -1,8 +1,9 @@
 #!/bin/bash
 # Profiling recipe for the headline bench (run on the GPU box from the repo root):
 #   bash bench/profile.sh <tag>
-# 1. rocprofv3 --kernel-trace --stats over the default-size bench (1M quicknet rounds, one stream) -> the
-#    per-kernel average durations that bench.py's live HIP-event roofline must agree with;
+# 1. rocprofv3 --kernel-trace --stats over the default bench command (1M quicknet rounds, 3 batches in flight,
+#    then bench.py's 2 single-stream roofline batches) -> bench/rocpd_stats.py --last 2 gives the per-kernel
+#    average over exactly the launches bench.py's HIP-event roofline measures;
 # 2. three separate --pmc passes (FETCH_SIZE, WRITE_SIZE, SQ instruction mix) over a 262144-round batch,
 #    one counter group per run as MI355X_MICROARCH.md prescribes (TCC: FETCH_SIZE uses 3 of 4 counters).
 # Each step has its own time limit; the first failure ends the script.
@@ -13,8 +14,8 @@ O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$TAG" -o run --output-format csv -- \
-  python3 "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --streams 1 > "$O/prof_$TAG.log" 2>&1
-SMALL="--rounds 262144 --steps 1 --warmup 0 --streams 1 --no-cpu-baseline"
+  python3 "$R/bench.py" --steps 6 --warmup 1 --no-cpu-baseline > "$O/prof_$TAG.log" 2>&1
+SMALL="--rounds 262144 --steps 1 --warmup 0 --streams 1 --roofline-steps 0 --no-cpu-baseline"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch_$TAG" -o pmc --output-format csv -- python3 "$R/bench.py" $SMALL \
   > "$O/pmc_fetch_$TAG.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write_$TAG" -o pmc --output-format csv -- python3 "$R/bench.py" $SMALL \
