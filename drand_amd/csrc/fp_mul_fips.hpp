@@ -243,12 +243,102 @@ __device__ __forceinline__ void fips_mont_mul(uint32_t r[12], const uint32_t a[1
   fips_final_sub(r, acc, P);
 }
 
-__device__ __forceinline__ void fips_mont_sqr(uint32_t r[12], const uint32_t a[12]) {
+__device__ __forceinline__ void fips_mont_sqr_col(uint32_t r[12], const uint32_t a[12]) {
   const uint32_t P[12] = DH_P_LIMBS;
   uint32_t m[12];
   uint64_t acc = 0;
   uint32_t hi = 0;
   sqr_cols(std::make_integer_sequence<int, 23>{}, acc, hi, m, r, a, P);
+  fips_final_sub(r, acc, P);
+}
+// Squaring, three phases: (1) the off-diagonal triangle T = sum_{i<j} a_i a_j 2^(32(i+j)) by product scanning
+// (66 products, no per-column doubling), (2) 2T word by word with one v_alignbit each, (3) Montgomery
+// product scanning over 2T + the diagonal squares, where each column's incoming word is added in the same
+// two instructions that shift the accumulator (no separate 96-bit add). 222 products as in fips_mont_sqr_col,
+// ~25% fewer other instructions.
+template <int K>
+__device__ __forceinline__ void sqr_tri_col(uint64_t& acc, uint32_t& hi, uint32_t t[24], const uint32_t a[12]) {
+  constexpr int LO = K > 11 ? K - 11 : 0;
+  constexpr int D = (K + 1) / 2 - LO > 0 ? (K + 1) / 2 - LO : 0;  // pairs i < K-i, i >= LO
+  if constexpr (D > 0) {
+    uint32_t xs[D], ys[D];
+#pragma unroll
+    for (int j = 0; j < D; j++) { xs[j] = a[LO + j]; ys[j] = a[K - LO - j]; }
+    mac_n<D>(acc, hi, xs, ys);
+  }
+  t[K] = (uint32_t)acc;
+  acc = (acc >> 32) | ((uint64_t)hi << 32);
+  hi = 0;
+}
+
+// acc <- (hi:acc_hi) + w, i.e. shift the 96-bit column accumulator down one word and add the next input word
+__device__ __forceinline__ void acc_shift_add(uint64_t& acc, uint32_t& hi, uint32_t w) {
+  uint32_t lo = (uint32_t)(acc >> 32), h = hi;
+  uint64_t c_;
+  asm volatile("v_add_co_u32_e64 %0, %2, %0, %3\n\tv_addc_co_u32_e64 %1, %2, %1, 0, %2"
+               : "+v"(lo), "+v"(h), "=&s"(c_)
+               : "v"(w));
+  acc = (uint64_t)lo | ((uint64_t)h << 32);
+  hi = 0;
+}
+
+template <int K>
+__device__ __forceinline__ void sqr_red_col(uint64_t& acc, uint32_t& hi, uint32_t m[12], uint32_t r[12], const uint32_t t[24],
+                                            const uint32_t a[12], const uint32_t P[12]) {
+  constexpr uint32_t NP0 = 0xfffcfffdu;
+  constexpr int LO = K > 11 ? K - 11 : 0, MUP = K < 12 ? K - 1 : 11;
+  constexpr int CM = MUP >= LO ? MUP - LO + 1 : 0;
+  constexpr int C = CM + ((K & 1) == 0 ? 1 : 0);
+  // word K of 2T
+  uint32_t u = K == 0 ? t[0] << 1 : __builtin_amdgcn_alignbit(t[K], t[K > 0 ? K - 1 : 0], 31);
+  if constexpr (K == 0) {
+    acc = u;
+    hi = 0;
+  } else {
+    acc_shift_add(acc, hi, u);
+  }
+  if constexpr (C > 0) {
+    uint32_t xs[C], ys[C];
+    int c = 0;
+    if constexpr ((K & 1) == 0) { xs[0] = a[K >> 1]; ys[0] = a[K >> 1]; c = 1; }
+#pragma unroll
+    for (int j = 0; j < CM; j++) { xs[c + j] = m[LO + j]; ys[c + j] = P[K - LO - j]; }
+    mac_n<C>(acc, hi, xs, ys);
+  }
+  if constexpr (K < 12) {
+    m[K] = (uint32_t)acc * NP0;
+    uint32_t p0 = P[0];
+    mac_n<1>(acc, hi, &m[K], &p0);
+  } else {
+    r[K - 12] = (uint32_t)acc;
+  }
+}
+
+template <int... K>
+__device__ __forceinline__ void sqr_tri_cols(std::integer_sequence<int, K...>, uint64_t& acc, uint32_t& hi, uint32_t t[24],
+                                             const uint32_t a[12]) {
+  (sqr_tri_col<K>(acc, hi, t, a), ...);
+}
+template <int... K>
+__device__ __forceinline__ void sqr_red_cols(std::integer_sequence<int, K...>, uint64_t& acc, uint32_t& hi, uint32_t m[12],
+                                             uint32_t r[12], const uint32_t t[24], const uint32_t a[12], const uint32_t P[12]) {
+  (sqr_red_col<K>(acc, hi, m, r, t, a, P), ...);
+}
+
+__device__ __forceinline__ void fips_mont_sqr(uint32_t r[12], const uint32_t a[12]) {
+  const uint32_t P[12] = DH_P_LIMBS;
+  uint32_t t[24], m[12];
+  uint64_t acc = 0;
+  uint32_t hi = 0;
+  t[0] = 0;
+  sqr_tri_cols(std::integer_sequence<int, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21>{},
+               acc, hi, t, a);
+  t[22] = (uint32_t)acc;
+  t[23] = (uint32_t)(acc >> 32);
+  acc = 0;
+  hi = 0;
+  sqr_red_cols(std::make_integer_sequence<int, 23>{}, acc, hi, m, r, t, a, P);
+  acc_shift_add(acc, hi, __builtin_amdgcn_alignbit(t[23], t[22], 31));
   fips_final_sub(r, acc, P);
 }
 #undef DH_P_LIMBS
