@@ -102,3 +102,55 @@ def check_past_beacons(store, scheme, pubkey, up_to, cb=None, window=1 << 20, se
         i += 1
     flush()
     return faulty
+
+
+class WrongBeaconID(Exception):
+    pass
+
+
+def sync_from_stream(packets, scheme, pubkey, store, up_to, beacon_id="", window=500, seed=0):
+    """tryNode's receive loop (/root/reference/chain/beacon/sync_manager.go:376-445) with verify-ahead windows
+    (SURVEY.md §8f row 4): packets arrive in order; up to `window` of them (the 500-deep gRPC buffer,
+    /root/reference/net/client_grpc.go:209) are verified in one batch, then stored in order until the first
+    packet that has the wrong beacon ID or fails verification (the serial loop stops at that packet, having
+    stored everything before it). Each packet is a dict {round, signature, previous_signature[, beacon_id]}.
+    Returns (done, stored rounds): done = the packet of round `up_to` was stored."""
+    stored = []
+    buf = []
+
+    def drain():
+        if not buf:
+            return None
+        n = len(buf)
+        rounds = np.array([int(p["round"]) for p in buf], dtype=np.uint64)
+        sigs = np.zeros((n, scheme.sig_len), dtype=np.uint8)
+        bad_len = np.zeros(n, dtype=bool)
+        for k, p in enumerate(buf):
+            if len(p["signature"]) == scheme.sig_len:
+                sigs[k] = np.frombuffer(bytes(p["signature"]), np.uint8)
+            else:
+                bad_len[k] = True
+        prevs = [bytes(p.get("previous_signature", b"")) for p in buf] if scheme.chained else None
+        ok, _ = scheme.verify_beacons(pubkey, rounds, sigs, prevs, seed=seed, want_randomness=False)
+        for k, p in enumerate(buf):
+            if bad_len[k] or not ok[k]:
+                return False
+            store.put(int(p["round"]), bytes(p["signature"]))
+            stored.append(int(p["round"]))
+            if int(p["round"]) == up_to:
+                return True
+        buf.clear()
+        return None
+
+    for p in packets:
+        bid = p.get("beacon_id")
+        if bid is not None and bid != beacon_id:
+            r = drain()  # packets before the mismatch were received first and are processed first
+            return (bool(r), stored)
+        buf.append(p)
+        if len(buf) >= window:
+            r = drain()
+            if r is not None:
+                return (r, stored)
+    r = drain()
+    return (bool(r), stored)

@@ -217,3 +217,31 @@ def test_check_past_beacons_batch_caller(dh):
         want = sorted(per_delete + ([10, 11] if s.chained else [10]))
         assert check_past_beacons(st, s, pk, 24, window=3) == want
         assert check_past_beacons(st, s, pk, 9) == [x for x in per_delete if x <= 9]
+
+
+def test_readers_and_client_walk_on_device(dh, tmp_path):
+    """Chain readers feeding the device path: a bbolt trimmed file (tests/boltwrite.py) replayed by
+    check_past_beacons, and the batched strict-client trust walk (client/verify.go:109-168)."""
+    from boltwrite import write_bolt
+    from drand_amd.chain import Info
+    from drand_amd.client import BatchVerifyingClient, ClientError
+    from drand_amd.store import BoltTrimmedStore
+    from drand_amd.sync import check_past_beacons
+    c = json.load(open(os.path.join(GOLD, "chains.json")))["pedersen-bls-chained"]
+    s = dh.scheme_from_name("pedersen-bls-chained")
+    sigs = {r: bytes.fromhex(x) for r, x in zip(c["rounds"], c["sigs"])}
+    kv = {int(0).to_bytes(8, "big"): bytes.fromhex(c["prevs"][0])}
+    kv.update({int(r).to_bytes(8, "big"): sg for r, sg in sigs.items() if r != 7})
+    path = str(tmp_path / "chain.db")
+    write_bolt(path, b"beacons", kv)
+    assert check_past_beacons(BoltTrimmedStore(path, True), s, bytes.fromhex(c["pk"]), 1000, window=8) == [7, 8]
+    info = Info(bytes.fromhex(c["pk"]), 30, s.name, 0, bytes.fromhex(c["prevs"][0]))
+    cl = BatchVerifyingClient(info, s, get_signature=lambda r: sigs[r], strict=True)
+    cl.point_of_trust = (3, sigs[3])
+    assert cl.trusted_previous_signature(20) == sigs[19] and cl.point_of_trust == (19, sigs[19])
+    bad = dict(sigs)
+    bad[15] = sigs[16]
+    cl2 = BatchVerifyingClient(info, s, get_signature=lambda r: bad[r], strict=True)
+    cl2.point_of_trust = (11, sigs[11])
+    with pytest.raises(ClientError):
+        cl2.trusted_previous_signature(20)
