@@ -33,9 +33,12 @@ SIGNATURES = {
     "dh_verify_beacon": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_size_t, _c.c_uint64, _c.c_char_p, _c.c_size_t,
                                     _c.c_char_p, _c.c_size_t]),
     "dh_verify_recovered": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_size_t, _c.c_char_p, _c.c_char_p, _c.c_size_t]),
+    "dh_verify_recovered_batch": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_size_t, _P, _P, _c.c_size_t, _c.c_size_t, _P,
+                                             _c.c_uint64]),
     "dh_digest_batch": (_c.c_int, [_c.c_int, _P, _P, _c.c_size_t, _P, _c.c_size_t, _P]),
     "dh_randomness_batch": (_c.c_int, [_c.c_int, _P, _c.c_size_t, _c.c_size_t, _P]),
     "dh_recover_batch": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_int, _c.c_int, _P, _P, _P, _c.c_size_t, _P, _P]),
+    "dh_verify_partials_batch": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_int, _c.c_int, _P, _P, _P, _c.c_size_t, _P]),
     "dh_sign_batch": (_c.c_int, [_c.c_int, _c.c_char_p, _P, _P, _c.c_size_t, _P, _c.c_size_t, _P]),
     "dh_public_key": (_c.c_int, [_c.c_int, _c.c_char_p, _P]),
     "dh_profile": (_c.c_int, [_c.c_int]),

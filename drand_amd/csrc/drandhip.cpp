@@ -335,7 +335,8 @@ struct timed_launches {
 // core pipeline on device-resident inputs
 int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                 size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
-                uint8_t* d_verdict, uint8_t* d_rand, uint64_t seed, hipStream_t st, uint64_t* stats) {
+                uint8_t* d_verdict, uint8_t* d_rand, uint64_t seed, hipStream_t st, uint64_t* stats,
+                const uint8_t* d_msgs32 = nullptr) {
   const bool g2 = sig_on_g2(scheme);
   const int sig_len = g2 ? 96 : 48, key_len = g2 ? 48 : 96;
   if ((int)pk_len != key_len) return fail(DH_EINVAL, "public key must be %d bytes for scheme %d", key_len, scheme);
@@ -374,10 +375,16 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>" : "k_prep_sig<fp>", [&] {
     return dh::launch_prep(g2, d_sigs, sig_stride, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), d_rand, st);
   }));
-  HIP_TRY(T.run(g2 ? "k_prep_msg<fp2>" : "k_prep_msg<fp>", [&] {
-    return dh::launch_msg(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, n, scheme == DH_SCHEME_CHAINED && d_prevs ? 1 : 0,
-                          dst_id(scheme), w->q_pts.as<uint32_t>(), st);
-  }));
+  if (d_msgs32) {  // VerifyRecovered: the messages are given (32-byte digests), not derived from rounds
+    HIP_TRY(T.run(g2 ? "k_prep_msg32<fp2>" : "k_prep_msg32<fp>", [&] {
+      return dh::launch_msg32(g2, d_msgs32, n, dst_id(scheme), w->q_pts.as<uint32_t>(), st);
+    }));
+  } else {
+    HIP_TRY(T.run(g2 ? "k_prep_msg<fp2>" : "k_prep_msg<fp>", [&] {
+      return dh::launch_msg(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, n,
+                            scheme == DH_SCHEME_CHAINED && d_prevs ? 1 : 0, dst_id(scheme), w->q_pts.as<uint32_t>(), st);
+    }));
+  }
   uint32_t seedw[8];
   int rc = make_seed(seed, seedw);
   if (rc) return rc;
@@ -606,7 +613,7 @@ void lagrange_at_zero(const std::vector<uint32_t>& idx, uint32_t* out /* t x 8 w
 
 int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
                  const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* sig_out, uint8_t* status_out,
-                 hipStream_t st) {
+                 hipStream_t st, uint8_t* partial_ok_out = nullptr) {
   const bool g2 = sig_on_g2(scheme);
   const int sl = g2 ? 96 : 48, kl = g2 ? 48 : 96;
   const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1, aw = jw * 2 / 3;
@@ -760,6 +767,10 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     }));
     HIP_TRY(hipMemcpyAsync(ok.data(), w->r_ok.p, np, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+  }
+  if (partial_ok_out) {  // dh_verify_partials_batch: per-partial VerifyPartial verdicts only
+    memcpy(partial_ok_out, ok.data(), np);
+    return DH_OK;
   }
   // 12. selection (first t valid in the given order; sorted by index; duplicates dropped) + Lagrange sets
   std::vector<uint32_t> sel(n_rounds * (size_t)t, 0), lamset(n_rounds, 0);
@@ -984,10 +995,41 @@ int dh_verify_beacon(int scheme, const uint8_t* pk, size_t pk_len, uint64_t roun
   return rc < 0 ? rc : verdict;
 }
 
+int dh_verify_recovered_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* msgs32, const uint8_t* sigs,
+                              size_t sig_stride, size_t n, uint8_t* verdict_out, uint64_t seed) {
+  if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
+  if (!pk || (n && (!msgs32 || !sigs || !verdict_out))) return fail(DH_EINVAL, "null argument");
+  if (n == 0) return DH_OK;
+  lease L;
+  if (L.rc) return L.rc;
+  worker* w = L.w;
+  int rc = set_device_and_stream(w);
+  if (rc) return rc;
+  hipStream_t st = w->stream;
+  HIP_TRY(w->in_sigs.ensure(n * sig_stride));
+  HIP_TRY(w->r_msgs.ensure(n * 32));
+  HIP_TRY(w->out_verdict.ensure(n));
+  HIP_TRY(hipMemcpyAsync(w->in_sigs.p, sigs, n * sig_stride, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->r_msgs.p, msgs32, n * 32, hipMemcpyHostToDevice, st));
+  rc = verify_core(w, scheme, pk, pk_len, nullptr, w->in_sigs.as<uint8_t>(), sig_stride, nullptr, 0, nullptr, n,
+                   w->out_verdict.as<uint8_t>(), nullptr, seed, st, nullptr, w->r_msgs.as<uint8_t>());
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(verdict_out, w->out_verdict.p, n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return DH_OK;
+}
+
 int dh_verify_recovered(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* msg32, const uint8_t* sig,
                         size_t sig_len) {
-  (void)scheme; (void)pk; (void)pk_len; (void)msg32; (void)sig; (void)sig_len;
-  return fail(DH_EINVAL, "dh_verify_recovered: not yet implemented on the device path");
+  int sl = dh_sig_len(scheme);
+  if (sl < 0) return sl;
+  if (!msg32) return fail(DH_EINVAL, "null argument");
+  if (!sig || sig_len != (size_t)sl) return 0;  // kyber: wrong-length signature is an invalid signature
+  uint8_t sbuf[96] __attribute__((aligned(16)));
+  memcpy(sbuf, sig, sig_len);
+  uint8_t verdict = 0;
+  int rc = dh_verify_recovered_batch(scheme, pk, pk_len, msg32, sbuf, (size_t)sl, 1, &verdict, 0);
+  return rc < 0 ? rc : verdict;
 }
 
 int dh_digest_batch(int scheme, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride,
@@ -1046,6 +1088,23 @@ int dh_recover_batch(int scheme, const uint8_t* commits, int t, int n_nodes, con
   if (rc) return rc;
   return recover_core(L.w, scheme, commits, t, n_nodes, msgs32, partials, part_off, n_rounds, sig_out, status_out,
                       L.w->stream);
+}
+
+int dh_verify_partials_batch(int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
+                             const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* ok_out) {
+  if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
+  if (t < 1 || n_nodes < 1 || n_nodes > 65535 || !commits || (n_rounds && (!msgs32 || !partials || !part_off || !ok_out)))
+    return fail(DH_EINVAL, "bad VerifyPartial arguments");
+  for (size_t j = 0; j < n_rounds; j++)
+    if (part_off[j + 1] < part_off[j]) return fail(DH_EINVAL, "part_off must be non-decreasing");
+  if (n_rounds == 0 || part_off[n_rounds] == part_off[0]) return DH_OK;
+  lease L;
+  if (L.rc) return L.rc;
+  int rc = set_device_and_stream(L.w);
+  if (rc) return rc;
+  std::vector<uint8_t> status(n_rounds);
+  return recover_core(L.w, scheme, commits, t, n_nodes, msgs32, partials, part_off, n_rounds, nullptr, status.data(),
+                      L.w->stream, ok_out);
 }
 
 static void sk_words(const uint8_t* sk32, uint32_t w[8]) {

@@ -100,12 +100,37 @@ class Scheme:
         return verdict.astype(bool), rand
 
     # ---- threshold BLS (kyber sign/tbls as used at chain/beacon/chainstore.go:202,207)
-    def recover_batch(self, commits, t, n, msgs, partials_per_round):
-        """Batch tbls Recover. commits: t compressed key-group points (PubPoly commits, index 0 = group key);
-        msgs: per-round 32-byte messages (DigestBeacon); partials_per_round: per round a list of
-        (2-byte BE share index || signature) records, in arrival order.
-        Returns (signatures (n_rounds, sig_len) uint8, ok (n_rounds,) bool) where ok[j] is False when
-        fewer than t valid partials were given (Go: "not enough good public shares")."""
+    def verify_recovered(self, pubkey, msg, sig):
+        """ThresholdScheme.VerifyRecovered(public, msg, sig) (chain/beacon/chainstore.go:207): raises SchemeError
+        if sig is not a valid signature of the 32-byte msg under pubkey."""
+        if len(msg) != 32:
+            raise SchemeError("messages must be 32-byte digests")
+        rc = _lib.load().dh_verify_recovered(self.id, bytes(pubkey), len(pubkey), bytes(msg), bytes(sig), len(sig))
+        if _check(rc) != 1:
+            raise SchemeError("bls: invalid signature")
+
+    def verify_recovered_batch(self, pubkey, msgs, signatures, seed=0):
+        """VerifyRecovered for n (32-byte msg, signature) pairs in one batch: (n,) bool verdicts."""
+        n = len(msgs)
+        m = np.frombuffer(b"".join(bytes(x) for x in msgs), dtype=np.uint8).copy() if n else np.zeros(0, np.uint8)
+        if len(m) != 32 * n:
+            raise SchemeError("messages must be 32-byte digests")
+        sigs = np.ascontiguousarray(signatures, dtype=np.uint8)
+        if sigs.shape != (n, self.sig_len):
+            raise SchemeError("signatures must be (%d, %d)" % (n, self.sig_len))
+        verdict = np.zeros(n, dtype=np.uint8)
+        _check(_lib.load().dh_verify_recovered_batch(self.id, bytes(pubkey), len(pubkey), _ptr(m), _ptr(sigs),
+                                                     self.sig_len, n, _ptr(verdict), int(seed)))
+        return verdict.astype(bool)
+
+    def index_of(self, partial):
+        """ThresholdScheme.IndexOf (chain/beacon/node.go:133): the 2-byte big-endian share index."""
+        partial = bytes(partial)
+        if len(partial) < 2:
+            raise SchemeError("invalid partial signature")
+        return int.from_bytes(partial[:2], "big")
+
+    def _pack_partials(self, commits, t, msgs, partials_per_round):
         commits = b"".join(bytes(c) for c in commits)
         if len(commits) != t * self.key_len:
             raise SchemeError("need t commitments of %d bytes" % self.key_len)
@@ -124,6 +149,30 @@ class Scheme:
                 blobs.append(p)
             off[j + 1] = len(blobs)
         raw = np.frombuffer(b"".join(blobs), dtype=np.uint8).copy() if blobs else np.zeros(rec, np.uint8)
+        return commits, m, raw, off, len(blobs)
+
+    def verify_partials_batch(self, commits, t, n, msgs, partials_per_round):
+        """Batch VerifyPartial (chain/beacon/node.go:150): per round, each (index || sig) partial checked against
+        PubPoly.Eval(index) for that round's 32-byte message. Returns a list (per round) of bool arrays."""
+        commits, m, raw, off, npart = self._pack_partials(commits, t, msgs, partials_per_round)
+        ok = np.zeros(max(npart, 1), dtype=np.uint8)
+        _check(_lib.load().dh_verify_partials_batch(self.id, commits, int(t), int(n), _ptr(m), _ptr(raw), _ptr(off),
+                                                    len(msgs), _ptr(ok)))
+        return [ok[off[j]:off[j + 1]].astype(bool) for j in range(len(msgs))]
+
+    def verify_partial(self, commits, t, n, msg, partial):
+        """ThresholdScheme.VerifyPartial(pubPoly, msg, partial): raises SchemeError when invalid."""
+        if not self.verify_partials_batch(commits, t, n, [msg], [[partial]])[0][0]:
+            raise SchemeError("bls: invalid partial signature")
+
+    def recover_batch(self, commits, t, n, msgs, partials_per_round):
+        """Batch tbls Recover. commits: t compressed key-group points (PubPoly commits, index 0 = group key);
+        msgs: per-round 32-byte messages (DigestBeacon); partials_per_round: per round a list of
+        (2-byte BE share index || signature) records, in arrival order.
+        Returns (signatures (n_rounds, sig_len) uint8, ok (n_rounds,) bool) where ok[j] is False when
+        fewer than t valid partials were given (Go: "not enough good public shares")."""
+        commits, m, raw, off, _ = self._pack_partials(commits, t, msgs, partials_per_round)
+        n_rounds = len(msgs)
         sigs = np.zeros((n_rounds, self.sig_len), dtype=np.uint8)
         ok = np.zeros(n_rounds, dtype=np.uint8)
         _check(_lib.load().dh_recover_batch(self.id, commits, int(t), int(n), _ptr(m), _ptr(raw), _ptr(off), n_rounds,

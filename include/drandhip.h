@@ -85,9 +85,20 @@ int dh_verify_batch_device(int scheme, const uint8_t* pk, size_t pk_len, const u
 int dh_verify_beacon(int scheme, const uint8_t* pk, size_t pk_len, uint64_t round, const uint8_t* sig, size_t sig_len,
                      const uint8_t* prev, size_t prev_len);
 
-/* ThresholdScheme.VerifyRecovered(pk, msg, sig) for a 32-byte msg (a beacon digest): 1 / 0 / < 0 */
+/*
+ * ThresholdScheme.VerifyRecovered(pk, msg, sig) (kyber sign/tbls = bls.Verify; called at
+ * chain/beacon/chainstore.go:207 on every recovered signature) for a 32-byte msg (a beacon digest):
+ * 1 valid / 0 invalid / < 0 error.
+ */
 int dh_verify_recovered(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* msg32, const uint8_t* sig,
                         size_t sig_len);
+
+/*
+ * Batch VerifyRecovered: n (32-byte digest, signature) pairs under one key, host buffers, same batching and
+ * bit-exact per-item verdicts as dh_verify_batch (verdict_out[i] = 1 valid, 0 invalid).
+ */
+int dh_verify_recovered_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* msgs32, const uint8_t* sigs,
+                              size_t sig_stride, size_t n, uint8_t* verdict_out, uint64_t seed);
 
 /* crypto.Scheme.DigestBeacon for n rounds (host-side SHA-256, no device): out n*32 bytes */
 int dh_digest_batch(int scheme, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride,
@@ -107,6 +118,15 @@ int dh_randomness_batch(int scheme, const uint8_t* sigs, size_t sig_stride, size
 int dh_recover_batch(int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
                      const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* sig_out,
                      uint8_t* status_out);
+
+/*
+ * Batch ThresholdScheme.VerifyPartial(pubPoly, msg, partial) (kyber sign/tbls; called per incoming partial at
+ * chain/beacon/node.go:150): same input layout as dh_recover_batch; ok_out[k] (one byte per partial, in
+ * input order) = 1 when the k-th partial's signature verifies under PubPoly.Eval(index) for its round's
+ * message, 0 otherwise. Indices >= n_nodes have no share in the group and are reported invalid.
+ */
+int dh_verify_partials_batch(int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
+                             const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* ok_out);
 
 /*
  * Synthetic-chain utilities (test fixtures and benchmark inputs; not part of the verification path):

@@ -245,3 +245,34 @@ def test_readers_and_client_walk_on_device(dh, tmp_path):
     cl2.point_of_trust = (11, sigs[11])
     with pytest.raises(ClientError):
         cl2.trusted_previous_signature(20)
+
+
+@pytest.mark.parametrize("scheme", ["pedersen-bls-unchained", "bls-unchained-g1-rfc9380"])
+def test_verify_partials_and_recovered(dh, scheme, oracle):
+    """Batch VerifyPartial (chain/beacon/node.go:150) per partial against the oracle's
+    Verify(PubPoly.Eval(i), msg, sig), and VerifyRecovered (chainstore.go:207) on the golden recovered
+    signatures, a swapped message and a wrong-length signature."""
+    c = json.load(open(os.path.join(GOLD, "recover.json")))[scheme]
+    s = dh.scheme_from_name(scheme)
+    commits = [bytes.fromhex(x) for x in c["commits"]]
+    msgs = [bytes.fromhex(x["msg"]) for x in c["cases"]]
+    parts = [[bytes.fromhex(p) for p in x["partials"]] for x in c["cases"]]
+    got = s.verify_partials_batch(commits, c["t"], c["n"], msgs, parts)
+    n_bad = 0
+    for j, ps in enumerate(parts):
+        for k, p in enumerate(ps):
+            i = s.index_of(p)
+            want = i < c["n"] and oracle.verify(scheme, oracle.pubpoly_eval(scheme, commits, i), msgs[j], p[2:])
+            assert bool(got[j][k]) == bool(want), (j, k)
+            n_bad += not want
+    assert n_bad > 0
+    good = [(bytes.fromhex(x["msg"]), bytes.fromhex(x["expected"])) for x in c["cases"] if x["expected"]]
+    for m, sig in good:
+        s.verify_recovered(commits[0], m, sig)
+    with pytest.raises(dh.SchemeError):
+        s.verify_recovered(commits[0], good[1][0], good[0][1])
+    with pytest.raises(dh.SchemeError):
+        s.verify_recovered(commits[0], good[0][0], good[0][1][:-1])
+    ms = [m for m, _ in good] + [good[1][0]]
+    sg = np.array([np.frombuffer(x, np.uint8) for _, x in good] + [np.frombuffer(good[0][1], np.uint8)])
+    assert s.verify_recovered_batch(commits[0], ms, sg, seed=4).tolist() == [True] * len(good) + [False]
