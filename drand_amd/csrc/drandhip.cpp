@@ -87,6 +87,8 @@ struct worker {
   dbuf key_raw, key_aff, key_ok;
   // MSM
   dbuf cnt, off, scan_tmp, list, buckets, segs, outA, outB, out2, pass, part, meta;
+  // lane-parallel pairing checks
+  dbuf vm_pairs, vm_live, vm_done;
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
@@ -101,7 +103,7 @@ struct worker {
   void release_all() {
     dbuf* all[] = {&status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
-                   &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &r_commits, &r_cstatus, &r_caff, &r_shares,
+                   &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
                    &r_sigbytes, &r_status2, &r_aff2, &r_entries2};
@@ -332,6 +334,37 @@ struct timed_launches {
   ~timed_launches() { resolve(); }
 };
 
+// Pairing checks: the lane-parallel program (k_vm.hip) unless DRANDHIP_LANE_PAIRING=1 selects the one-lane
+// tower code (k_check.hip), kept as the independent second implementation the parity tests compare against.
+static bool lane_pairing() {
+  static const bool v = [] {
+    const char* e = getenv("DRANDHIP_LANE_PAIRING");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+static hipError_t group_check(worker* w, bool g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key,
+                              uint8_t* pass, hipStream_t st) {
+  if (lane_pairing()) return dh::launch_group_check(g2, A, B, ngroups, key, pass, st);
+  hipError_t e;
+  if ((e = w->vm_pairs.ensure(ngroups * 2 * 72 * 4)) != hipSuccess) return e;
+  if ((e = w->vm_live.ensure(ngroups * 2)) != hipSuccess) return e;
+  return dh::launch_group_check_vm(g2, A, B, ngroups, key, w->vm_pairs.as<uint32_t>(), w->vm_live.as<uint8_t>(), pass, st);
+}
+
+static hipError_t leaf_check(worker* w, bool g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff,
+                             const uint32_t* q_pts, const uint32_t* key, const uint8_t* status, uint8_t* verdict,
+                             hipStream_t st) {
+  if (lane_pairing()) return dh::launch_leaf_check(g2, entries, m, sig_aff, q_pts, key, status, verdict, st);
+  hipError_t e;
+  if ((e = w->vm_pairs.ensure(m * 2 * 72 * 4)) != hipSuccess) return e;
+  if ((e = w->vm_live.ensure(m * 2)) != hipSuccess) return e;
+  if ((e = w->vm_done.ensure(m)) != hipSuccess) return e;
+  return dh::launch_leaf_check_vm(g2, entries, m, sig_aff, q_pts, key, status, w->vm_pairs.as<uint32_t>(),
+                                  w->vm_live.as<uint8_t>(), w->vm_done.as<uint8_t>(), verdict, st);
+}
+
 // core pipeline on device-resident inputs
 int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                 size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
@@ -434,8 +467,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
                             w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st);
     }));
     HIP_TRY(T.run(level == 0 ? "k_group_check_level0" : "k_group_check_bisect", [&] {
-      return dh::launch_group_check(g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups,
-                                    w->key_aff.as<uint32_t>(), w->pass.as<uint8_t>(), st);
+      return group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups, w->key_aff.as<uint32_t>(),
+                         w->pass.as<uint8_t>(), st);
     }));
     HIP_TRY(dh::launch_mark_groups(w->entries.as<uint32_t>(), m, gsize, w->pass.as<uint8_t>(), w->status.as<uint8_t>(),
                                    d_verdict, st));
@@ -463,8 +496,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   }
   if (m > 0) {
     HIP_TRY(T.run("k_leaf_check", [&] {
-      return dh::launch_leaf_check(g2, w->entries.as<uint32_t>(), m, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
-                                   w->key_aff.as<uint32_t>(), w->status.as<uint8_t>(), d_verdict, st);
+      return leaf_check(w, g2, w->entries.as<uint32_t>(), m, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
+                        w->key_aff.as<uint32_t>(), w->status.as<uint8_t>(), d_verdict, st);
     }));
     if (stats) stats[2] = m;
   }
@@ -859,8 +892,8 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
                                     w->r_aff2.as<uint32_t>(), w->r_q.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
                                     w->outB.as<uint32_t>(), st);
       if (e != hipSuccess) return e;
-      return dh::launch_group_check(g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), 1, w->key_aff.as<uint32_t>(),
-                                    w->pass.as<uint8_t>(), st);
+      return group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), 1, w->key_aff.as<uint32_t>(),
+                         w->pass.as<uint8_t>(), st);
     }));
     uint8_t pass = 0, dummy = 0;
     (void)dummy;
@@ -871,9 +904,8 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
       HIP_TRY(hipMemcpyAsync(vv.data(), w->r_status2.p, n_rounds, hipMemcpyDeviceToHost, st));
     } else {
       HIP_TRY(hipMemsetAsync(w->r_ok.p, 0, n_rounds, st));
-      HIP_TRY(dh::launch_leaf_check(g2, w->r_entries2.as<uint32_t>(), n_rounds, w->r_aff2.as<uint32_t>(),
-                                    w->r_q.as<uint32_t>(), w->key_aff.as<uint32_t>(), w->r_status2.as<uint8_t>(),
-                                    w->r_ok.as<uint8_t>(), st));
+      HIP_TRY(leaf_check(w, g2, w->r_entries2.as<uint32_t>(), n_rounds, w->r_aff2.as<uint32_t>(), w->r_q.as<uint32_t>(),
+                         w->key_aff.as<uint32_t>(), w->r_status2.as<uint8_t>(), w->r_ok.as<uint8_t>(), st));
       HIP_TRY(hipMemcpyAsync(vv.data(), w->r_ok.p, n_rounds, hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipStreamSynchronize(st));

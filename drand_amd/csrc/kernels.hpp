@@ -66,6 +66,13 @@ hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, c
 hipError_t launch_leaf_check(int sig_g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
                              const uint32_t* key_aff, const uint8_t* status, uint8_t* verdict, hipStream_t st);
 
+// lane-parallel pairing checks (k_vm.hip): pairs = 2 x 72 words per check, live = 2 bytes, done = 1 byte
+hipError_t launch_group_check_vm(int sig_g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_aff,
+                                 uint32_t* pairs, uint8_t* live, uint8_t* pass, hipStream_t st);
+hipError_t launch_leaf_check_vm(int sig_g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
+                                const uint32_t* key_aff, const uint8_t* status, uint32_t* pairs, uint8_t* live, uint8_t* done,
+                                uint8_t* verdict, hipStream_t st);
+
 hipError_t launch_sign(int sig_g2, const uint32_t* sk, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride,
                        const uint32_t* prev_lens, size_t n, int chained, int dst_id, uint8_t* out, hipStream_t st);
 hipError_t launch_pubkey(int key_g2, const uint32_t* sk, uint8_t* out, hipStream_t st);

@@ -276,3 +276,18 @@ def test_verify_partials_and_recovered(dh, scheme, oracle):
     ms = [m for m, _ in good] + [good[1][0]]
     sg = np.array([np.frombuffer(x, np.uint8) for _, x in good] + [np.frombuffer(good[0][1], np.uint8)])
     assert s.verify_recovered_batch(commits[0], ms, sg, seed=4).tolist() == [True] * len(good) + [False]
+
+
+def test_one_lane_pairing_path(dh):
+    """The one-lane tower pairing (k_check.hip, DRANDHIP_LANE_PAIRING=1) stays correct: same verdicts as the
+    fixtures on the negative sets (group checks fail, bisection reaches per-round leaves)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, DRANDHIP_LANE_PAIRING="1")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "lane_pairing_check.py")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    neg = json.load(open(os.path.join(GOLD, "negatives.json")))
+    for name, v in got.items():
+        assert v == [x["valid"] for x in neg[name]["cases"]], name
