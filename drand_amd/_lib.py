@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdrandhip.so")
+LIB_PATH = os.environ.get("DRANDHIP_LIB") or os.path.join(HERE, "libdrandhip.so")
 
 DH_OK = 0
 DH_EINVAL = -1

@@ -30,8 +30,8 @@ import gen_consts as gc  # noqa: E402
 
 P = gc.P
 U_ABS = -gc.U
-MAXT = 6     # terms per operand / LIN op
-MAXC = 8     # |coefficient| per term
+MAXT = 7     # terms per operand / LIN op
+MAXC = 64     # |coefficient| per term
 LANES = 64
 
 
@@ -613,34 +613,46 @@ def validate(np_, prog, outs, phases, slot, nslots):
 
 
 # ----------------------------------------------------------------------------------------- emission
+REC = 16  # words per op record: header, MAXT A terms, MAXT B terms (fixed positions), padding
+
+
 def emit(progs):
-    """progs: list of (np, prog, outs, phases, slot, nslots). One constant pool shared by all programs."""
+    """progs: list of (np, prog, outs, phases, slot, nslots).
+
+    Layout read by k_vm.hip: PHASES[2 * ph] = kind | cnt << 8, PHASES[2 * ph + 1] = index of the phase's first op;
+    op k of phase ph is the REC-word record OPS[REC * (first + k) ...]: word 0 = dst slot | na << 16 | nb << 24,
+    words 1..MAXT = A terms, words 1+MAXT..2*MAXT = B terms, a term = slot | (coeff & 0xffff) << 16."""
+    assert 1 + 2 * MAXT <= REC
     lines = ["// generated by drand_amd/tools/gen_pairing_vm.py — do not edit",
              "// Lane-parallel multi-pairing check programs (see the generator's docstring).",
              "#pragma once", "#include <stdint.h>", "", "namespace dh {", "namespace vm {", ""]
-    lines.append("constexpr int MAXT = %d;" % MAXT)
+    lines.append("constexpr int MAXT = %d, MAXC = %d, REC = %d;" % (MAXT, MAXC, REC))
     lines.append("enum : uint32_t { PH_MUL = 0, PH_LIN = 1, PH_INV = 2 };")
-    lines.append("// op words: [0] = dst slot | na << 16 | nb << 24, then na + nb terms (slot | (coeff & 0xffff) << 16)")
     lines.append("")
     for np_, prog, outs, phases, slot, nslots in progs:
         nodes = prog.nodes
-        ph_words, op_words, op_off = [], [], []
+        ph_words, op_words = [], []
+        nops = 0
         for kind, batch in phases:
-            ph_words += [{"mul": 0, "lin": 1, "inv": 2}[kind], len(batch), len(op_off)]
+            ph_words += [{"mul": 0, "lin": 1, "inv": 2}[kind] | (len(batch) << 8), nops]
             for i in batch:
                 n = nodes[i]
                 a = n["a"]
                 b = n.get("b", [])
-                op_off.append(len(op_words))
-                op_words.append(slot[i] | (len(a) << 16) | (len(b) << 24))
-                for s, c in a + b:
-                    op_words.append(slot[s] | ((c & 0xffff) << 16))
+                rec = [0] * REC
+                rec[0] = slot[i] | (len(a) << 16) | (len(b) << 24)
+                for k, (s_, c) in enumerate(a):
+                    rec[1 + k] = slot[s_] | ((c & 0xffff) << 16)
+                for k, (s_, c) in enumerate(b):
+                    rec[1 + MAXT + k] = slot[s_] | ((c & 0xffff) << 16)
+                op_words += rec
+                nops += 1
         ins = [slot[i] for i in prog.inputs]
         consts = [(slot[n], v) for v, n in prog.consts.items() if n in slot]
         tag = "NP%d" % np_
         lines.append("// %s: %d phases (%d MUL, %d LIN, %d INV), %d ops, %d slots" % (
             tag, len(phases), sum(k == "mul" for k, _ in phases), sum(k == "lin" for k, _ in phases),
-            sum(k == "inv" for k, _ in phases), len(op_off), nslots))
+            sum(k == "inv" for k, _ in phases), nops, nslots))
         lines.append("constexpr int %s_NPHASES = %d, %s_NSLOTS = %d, %s_NCONST = %d;" % (
             tag, len(phases), tag, nslots, tag, len(consts)))
         lines.append("__device__ __constant__ uint32_t %s_INPUT_SLOT[%d] = {%s};" % (tag, len(ins), ", ".join(map(str, ins))))
@@ -650,8 +662,8 @@ def emit(progs):
         lines.append("__device__ __constant__ uint32_t %s_CONST_VAL[%d][12] = {%s};" % (
             tag, len(consts), ", ".join(gc.c_fp(v) for _, v in consts)))
         lines.append("__device__ const uint32_t %s_PHASES[%d] = {%s};" % (tag, len(ph_words), ", ".join(map(str, ph_words))))
-        lines.append("__device__ const uint32_t %s_OPOFF[%d] = {%s};" % (tag, len(op_off), ", ".join(map(str, op_off))))
-        lines.append("__device__ const uint32_t %s_OPS[%d] = {%s};" % (tag, len(op_words), ", ".join("0x%x" % w for w in op_words)))
+        lines.append("__device__ const uint32_t __attribute__((aligned(16))) %s_OPS[%d] = {%s};" % (
+            tag, len(op_words), ", ".join("0x%x" % w for w in op_words)))
         lines.append("")
     lines += ["}  // namespace vm", "}  // namespace dh", ""]
     return "\n".join(lines)
