@@ -750,9 +750,10 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(w->segs.ensure(std::max((size_t)gA.nwin * gA.nseg, (size_t)n_nodes * gB.nwin * gB.nseg) * jw * 4));
     HIP_TRY(w->outA.ensure(jw * 4));
     HIP_TRY(w->outB.ensure((size_t)n_nodes * jw * 4));
-    const size_t max_ent = std::max(np * gA.nwin, mB * gB.nwin);
-    HIP_TRY(w->part.ensure(dh::msm_part_bytes(max_ent, jw, 1)));
-    HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(max_ent)));
+    // chunk length depends on the list length: size for each of the two MSMs, not for the longer list
+    const size_t entA = np * gA.nwin, entB = mB * gB.nwin;
+    HIP_TRY(w->part.ensure(std::max(dh::msm_part_bytes(entA, jw, 1), dh::msm_part_bytes(entB, jw, 1))));
+    HIP_TRY(w->meta.ensure(std::max(dh::msm_meta_bytes(entA), dh::msm_meta_bytes(entB))));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
                   w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), nullptr, w->part.as<uint32_t>(),
                   w->meta.as<uint32_t>(), 0};
@@ -871,6 +872,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(dh::launch_scalars(d_seed, n_rounds, w->r_status2.as<uint8_t>(), w->r_scal.as<uint4>(), st));
     HIP_TRY(dh::launch_iota(w->r_entries2.as<uint32_t>(), n_rounds, st));
     // group key = commit 0 (affine, key group) — staged where the group check expects it
+    HIP_TRY(w->key_aff.ensure(48 * 4));
     HIP_TRY(hipMemcpyAsync(w->key_aff.p, w->r_caff.p, kaw * 4, hipMemcpyDeviceToDevice, st));
     w->cached_key_len = 0;  // key_aff now holds this call's key
     const dh::msm_geom g = geom_for(n_rounds);

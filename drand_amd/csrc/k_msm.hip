@@ -213,7 +213,7 @@ static hipError_t launch_buckets(const msm_ws& ws, size_t nk, const uint32_t* pt
   if (e != hipSuccess) return e;
   if (!ws.max_entries) return hipSuccess;
   const uint32_t L = msm_chunk_len(ws.max_entries);
-  const size_t nch = (ws.max_entries + L - 1) / L;
+  const size_t nch = (ws.max_entries + L - 1) / L;  // <= msm_nchunks(max_entries): the workspace bound
   hipLaunchKernelGGL((k_msm_bucket<F, AFFINE>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, pts, buckets,
                      part, write_meta ? ws.meta : nullptr);
   hipLaunchKernelGGL((k_msm_bucket_fix<F>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, nk, L, ws.meta, part, buckets);

@@ -12,6 +12,13 @@ from drand_amd import scheme_from_name  # noqa: E402
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 out = {}
+# Recover first in a fresh process (no earlier verify call has sized the key buffers)
+rc = json.load(open(os.path.join(GOLD, "recover.json")))["pedersen-bls-unchained"]
+s = scheme_from_name("pedersen-bls-unchained")
+sigs, ok = s.recover_batch([bytes.fromhex(x) for x in rc["commits"]], rc["t"], rc["n"],
+                           [bytes.fromhex(x["msg"]) for x in rc["cases"]],
+                           [[bytes.fromhex(p) for p in x["partials"]] for x in rc["cases"]])
+out["recover"] = [sigs[k].tobytes().hex() if ok[k] else None for k in range(len(rc["cases"]))]
 neg = json.load(open(os.path.join(GOLD, "negatives.json")))
 for name in ("bls-unchained-g1-rfc9380", "pedersen-bls-chained"):
     c = neg[name]

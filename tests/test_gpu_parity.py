@@ -280,7 +280,8 @@ def test_verify_partials_and_recovered(dh, scheme, oracle):
 
 def test_one_lane_pairing_path(dh):
     """The one-lane tower pairing (k_check.hip, DRANDHIP_LANE_PAIRING=1) stays correct: same verdicts as the
-    fixtures on the negative sets (group checks fail, bisection reaches per-round leaves)."""
+    fixtures on the negative sets (group checks fail, bisection reaches per-round leaves); the child process also
+    runs tbls Recover as its very first library call."""
     import subprocess
     import sys
     env = dict(os.environ, DRANDHIP_LANE_PAIRING="1")
@@ -288,6 +289,8 @@ def test_one_lane_pairing_path(dh):
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     got = json.loads(r.stdout.strip().splitlines()[-1])
+    rc = json.load(open(os.path.join(GOLD, "recover.json")))["pedersen-bls-unchained"]
+    assert got.pop("recover") == [x["expected"] for x in rc["cases"]]
     neg = json.load(open(os.path.join(GOLD, "negatives.json")))
     for name, v in got.items():
         assert v == [x["valid"] for x in neg[name]["cases"]], name
