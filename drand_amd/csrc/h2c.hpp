@@ -126,7 +126,7 @@ DH_DEV swu_out<fp2> sswu_g2(const fp2& u) {
   t2 = fp2_add(t2, fp2_mul(B, tv6));
   fp2 x = fp2_mul(tv1, tv3);
   fp2 y1;
-  bool gx1_sq = fp2_sqrt_ratio(y1, t2, tv6);
+  bool gx1_sq = fp2_sqrt_ratio_cm(y1, t2, tv6);
   fp2 y = fp2_mul(fp2_mul(tv1, u), y1);
   x = fp2_select(gx1_sq, tv3, x);
   y = fp2_select(gx1_sq, y1, y);

@@ -321,6 +321,11 @@ def main():
     fp2_const("SQRT_RATIO2_C6", c6)
     fp2_const("SQRT_RATIO2_C7", c7)
     fp_const("INV2", (P + 1) // 2)  # 1/2
+    # norm-based sqrt_ratio over Fp2 (fp2_sqrt_ratio_cm): N(Z) and N(Z)^((p-3)/4)
+    nz = (Z2[0] * Z2[0] + Z2[1] * Z2[1]) % P
+    fp_const("SSWU2_NZ", nz)
+    fp_const("SSWU2_NZ_K", pow(nz, (P - 3) // 4, P))
+    w("constexpr bool SIGMA_K_NEG = %s;  // (-1)^((p-3)/4) == -1" % ("true" if pow(P - 1, (P - 3) // 4, P) != 1 else "false"))
     fp_const("K256", k256)
     fp_const("K256R", k256 * MONT % P)  # mont_mul(raw hi, K256R) = Mont(hi * 2^256)
     fp_const("R2", MONT % P)  # c_fp(R) = R^2 mod p: mont_mul(raw x, R2) = Mont(x)
