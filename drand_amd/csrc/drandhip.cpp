@@ -613,8 +613,34 @@ void fr_to_words(const fr& a, uint32_t out[8]) {  // leave Montgomery form, litt
     out[2 * i + 1] = (uint32_t)(p.v[i] >> 32);
   }
 }
-// Lagrange basis at 0 over x_k = idx_k + 1 (share.RecoverCommit / lagrangeBasis [kyber v1.1.18 share/poly.go])
-void lagrange_at_zero(const std::vector<uint32_t>& idx, uint32_t* out /* t x 8 words */) {
+// non-adjacent form of a < 2^255 (little-endian 32-bit words): positive-digit mask, negative-digit mask
+// (256 positions each): ~1/3 of the positions are nonzero instead of ~1/2 of the bits
+static void naf_masks(const uint32_t w[8], uint32_t pos[8], uint32_t neg[8]) {
+  uint64_t k[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) k[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+  memset(pos, 0, 32);
+  memset(neg, 0, 32);
+  for (int b = 0; b < 257; b++) {
+    if (k[0] & 1) {
+      const bool minus = (k[0] & 3) == 3;  // digit -1: k += 1, else digit +1: k -= 1
+      if (b >= 256) break;                 // cannot happen for a < 2^255
+      if (minus) {
+        neg[b >> 5] |= 1u << (b & 31);
+        for (int i = 0; i < 5 && ++k[i] == 0; i++) {
+        }
+      } else {
+        pos[b >> 5] |= 1u << (b & 31);
+        k[0] -= 1;
+      }
+    }
+    for (int i = 0; i < 4; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 63);
+    k[4] >>= 1;
+  }
+}
+
+// Lagrange basis at 0 over x_k = idx_k + 1 (share.RecoverCommit / lagrangeBasis [kyber v1.1.18 share/poly.go]),
+// each coefficient as NAF masks: out[16 k .. 16 k + 7] positive digits, out[16 k + 8 .. 16 k + 15] negative
+void lagrange_at_zero(const std::vector<uint32_t>& idx, uint32_t* out /* t x 16 words */) {
   const size_t t = idx.size();
   std::vector<fr> den(t), num(t);
   for (size_t k = 0; k < t; k++) {
@@ -640,7 +666,9 @@ void lagrange_at_zero(const std::vector<uint32_t>& idx, uint32_t* out /* t x 8 w
   for (size_t k = t; k-- > 0;) {
     fr dk_inv = fr_mul(inv, pre[k]);
     inv = fr_mul(inv, den[k]);
-    fr_to_words(fr_mul(num[k], dk_inv), out + 8 * k);
+    uint32_t wds[8];
+    fr_to_words(fr_mul(num[k], dk_inv), wds);
+    naf_masks(wds, out + 16 * k, out + 16 * k + 8);
   }
 }
 
@@ -779,8 +807,13 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
       hipError_t e = dh::launch_recover_pairs(g2, w->r_shares.as<uint32_t>(), w->outB.as<uint32_t>(), w->outA.as<uint32_t>(),
                                               n_nodes, w->r_P.as<uint32_t>(), w->r_Q.as<uint32_t>(), st);
       if (e != hipSuccess) return e;
-      return dh::launch_pair_check(w->r_P.as<uint32_t>(), w->r_Q.as<uint32_t>(), npairs, 0, 0, nullptr, w->r_f.as<uint32_t>(),
-                                   w->r_skip.as<uint8_t>(), w->pass.as<uint8_t>(), st);
+      if (lane_pairing())
+        return dh::launch_pair_check(w->r_P.as<uint32_t>(), w->r_Q.as<uint32_t>(), npairs, 0, 0, nullptr,
+                                     w->r_f.as<uint32_t>(), w->r_skip.as<uint8_t>(), w->pass.as<uint8_t>(), st);
+      if ((e = w->vm_pairs.ensure(npairs * 72 * 4)) != hipSuccess) return e;
+      if ((e = w->vm_live.ensure(npairs)) != hipSuccess) return e;
+      return dh::launch_multi_pairing_vm(w->r_P.as<uint32_t>(), w->r_Q.as<uint32_t>(), npairs, w->vm_pairs.as<uint32_t>(),
+                                         w->vm_live.as<uint8_t>(), w->r_f.as<uint32_t>(), w->pass.as<uint8_t>(), st);
     }));
     uint8_t pass = 0;
     HIP_TRY(hipMemcpyAsync(&pass, w->pass.p, 1, hipMemcpyDeviceToHost, st));
@@ -832,8 +865,8 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
       sid = (uint32_t)sets.size();
       set_id.emplace(idx, sid);
       sets.push_back(idx);
-      lam.resize(lam.size() + (size_t)t * 8);
-      lagrange_at_zero(idx, lam.data() + (size_t)sid * t * 8);
+      lam.resize(lam.size() + (size_t)t * 16);
+      lagrange_at_zero(idx, lam.data() + (size_t)sid * t * 16);
     } else {
       sid = it->second;
     }
@@ -841,7 +874,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     lamset[j] = sid;
     rok[j] = 1;
   }
-  if (sets.empty()) lam.assign((size_t)t * 8, 0);
+  if (sets.empty()) lam.assign((size_t)t * 16, 0);
   // 13. interpolation on the device
   HIP_TRY(w->r_sel.ensure(sel.size() * 4));
   HIP_TRY(w->r_lam.ensure(lam.size() * 4));

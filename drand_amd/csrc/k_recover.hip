@@ -127,7 +127,7 @@ __global__ __launch_bounds__(64) void k_partial_leaf(const uint32_t* __restrict_
 // interpolation sum sum_k lambda_k sigma_k; the partial sums meet in LDS and the first lane of the round adds
 // them. One lane per round left most of the chip idle at 10^4-10^5 rounds and ran 33 terms x 127 additions
 // serially; four lanes cut the per-round latency ~3.8x for ~6% more doublings.
-constexpr int LG_LANES = 4;
+constexpr int LG_LANES = 4, LG_MAXK = 9;  // terms per lane and pass (t <= 36: one pass)
 template <class F>
 __global__ __launch_bounds__(64) void k_lagrange(const uint32_t* __restrict__ sel, const uint32_t* __restrict__ lam,
                                                  const uint32_t* __restrict__ lam_set, const uint8_t* __restrict__ ok,
@@ -135,18 +135,41 @@ __global__ __launch_bounds__(64) void k_lagrange(const uint32_t* __restrict__ se
                                                  uint32_t* __restrict__ out) {
   constexpr int JW = sizeof(F) / 4 * 3;
   __shared__ uint32_t part[64 * JW];
+  __shared__ uint32_t idxS[64][LG_MAXK], lpS[64][LG_MAXK], lnS[64][LG_MAXK];
   const size_t tid = gtid();
   const size_t j = tid / LG_LANES;
   const int q = (int)(tid % LG_LANES);
   jac<F> acc = jac_inf<F>();
   if (j < n_rounds && ok[j]) {
-    const uint32_t* L = lam + (size_t)lam_set[j] * t * 8;
+    const uint32_t* L = lam + (size_t)lam_set[j] * t * 16;  // per term: NAF positive mask, negative mask
     const uint32_t* S = sel + j * (size_t)t;
-    for (int b = 254; b >= 0; b--) {
-      acc = jac_dbl(acc);
-      for (int k = q; k < t; k += LG_LANES) {
-        if ((L[k * 8 + (b >> 5)] >> (b & 31)) & 1) acc = jac_add_aff(acc, ld_aff_aos<F>(sig_aff, S[k]));
+    const int nt = (t - q + LG_LANES - 1) / LG_LANES;  // terms of this lane: k = q + LG_LANES i
+    // digit masks of the current 32-bit chunk and the point indices live in LDS (dynamic indices, no scratch)
+    uint32_t* idx = idxS[threadIdx.x];
+    uint32_t* lp = lpS[threadIdx.x];
+    uint32_t* ln = lnS[threadIdx.x];
+    for (int c0 = 0; c0 < nt; c0 += LG_MAXK) {  // more than LG_MAXK terms: several passes
+      const int nc = nt - c0 < LG_MAXK ? nt - c0 : LG_MAXK;
+      jac<F> part_acc = jac_inf<F>();
+      for (int i = 0; i < nc; i++) idx[i] = S[q + LG_LANES * (c0 + i)];
+      for (int b = 255; b >= 0; b--) {
+        if ((b & 31) == 31)
+          for (int i = 0; i < nc; i++) {
+            const uint32_t* Lk = L + (size_t)(q + LG_LANES * (c0 + i)) * 16;
+            lp[i] = Lk[b >> 5];
+            ln[i] = Lk[8 + (b >> 5)];
+          }
+        part_acc = jac_dbl(part_acc);
+        for (int i = 0; i < nc; i++) {
+          const uint32_t pb = (lp[i] >> (b & 31)) & 1, nb = (ln[i] >> (b & 31)) & 1;
+          if (pb | nb) {
+            aff<F> pt = ld_aff_aos<F>(sig_aff, idx[i]);
+            if (nb) pt.y = f_neg(pt.y);
+            part_acc = jac_add_aff(part_acc, pt);
+          }
+        }
       }
+      acc = jac_add(acc, part_acc);
     }
   }
   st_jac_aos<F>(part, threadIdx.x, acc);

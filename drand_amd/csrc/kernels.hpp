@@ -73,6 +73,9 @@ hipError_t launch_leaf_check_vm(int sig_g2, const uint32_t* entries, size_t m, c
                                 const uint32_t* key_aff, const uint8_t* status, uint32_t* pairs, uint8_t* live, uint8_t* done,
                                 uint8_t* verdict, hipStream_t st);
 
+hipError_t launch_multi_pairing_vm(const uint32_t* P, const uint32_t* Q, size_t n, uint32_t* pairs, uint8_t* live,
+                                   uint32_t* f_tmp, uint8_t* pass, hipStream_t st);
+
 hipError_t launch_sign(int sig_g2, const uint32_t* sk, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride,
                        const uint32_t* prev_lens, size_t n, int chained, int dst_id, uint8_t* out, hipStream_t st);
 hipError_t launch_pubkey(int key_g2, const uint32_t* sk, uint8_t* out, hipStream_t st);

@@ -421,6 +421,40 @@ FROB6_C2 = [gc.f2pow(XI, 2 * (P ** k - 1) // 3) for k in (1, 2, 3)]
 FROB12_C = [gc.f2pow(XI, (P ** k - 1) // 6) for k in (1, 2, 3)]
 
 
+def _fp12_input(prefix):
+    c = [L.node(PROG.inp("%s%d" % (prefix, i))) for i in range(12)]
+    return F12(F6(F2(c[0], c[1]), F2(c[2], c[3]), F2(c[4], c[5])), F6(F2(c[6], c[7]), F2(c[8], c[9]), F2(c[10], c[11])))
+
+
+def build_tag(tag):
+    """Programs: NP1 / NP2 = the full check of 1 / 2 pairs; ML1 = the Miller loop of one pair (f out, for
+    multi-pairings of many pairs run one workgroup per pair); MUL12 = f * g; FE = final exponentiation."""
+    global PROG
+    if tag.startswith("NP"):
+        return build(int(tag[2:]))
+    PROG = Prog()
+    if tag == "ML1":
+        px, py = L.node(PROG.inp("P0.x")), L.node(PROG.inp("P0.y"))
+        qx = F2(L.node(PROG.inp("Q0.x0")), L.node(PROG.inp("Q0.x1")))
+        qy = F2(L.node(PROG.inp("Q0.y0")), L.node(PROG.inp("Q0.y1")))
+        r = miller_loop([(px, py)], [(qx, qy)])
+    elif tag == "MUL12":
+        r = _fp12_input("F") * _fp12_input("G")
+    elif tag == "FE":
+        r = final_exp(_fp12_input("F"))
+    else:
+        raise ValueError(tag)
+    outs = []
+    for c in r.coords():
+        m = c.mat()
+        if not m.t:
+            raise RuntimeError("zero output coordinate")
+        outs.append(m.single())
+    prog = PROG
+    PROG = None
+    return prog, outs
+
+
 def build(np_):
     global PROG
     PROG = Prog()
@@ -582,7 +616,40 @@ def _bls_points():
     return B
 
 
+def validate_split(progs):
+    """ML1 / MUL12 / FE composed must give the NP2 check: e(G1,G2) e(-G1,G2) = 1 and e(aP,Q) e(-P,aQ) = 1."""
+    B = _bls_points()
+    one = [1] + [0] * 11
+    run = {}
+    for tag, prog, outs, phases, slot, nslots in progs:
+        run[tag] = (lambda p=prog, o=outs, ph=phases, sl=slot, ns=nslots: (lambda inp: evaluate(p, o, ph, sl, ns, inp)))()
+
+    def ml(Pt, Qt):
+        return run["ML1"]({"P0.x": Pt[0], "P0.y": Pt[1], "Q0.x0": Qt[0][0], "Q0.x1": Qt[0][1],
+                           "Q0.y0": Qt[1][0], "Q0.y1": Qt[1][1]})
+
+    def mul(f, g):
+        d = {"F%d" % i: f[i] for i in range(12)}
+        d.update({"G%d" % i: g[i] for i in range(12)})
+        return run["MUL12"](d)
+
+    def fe(f):
+        return run["FE"]({"F%d" % i: f[i] for i in range(12)})
+
+    G1, G2 = B.G1_GEN, B.G2_GEN
+    a = random.Random(2).randrange(2, 1 << 64)
+    Pa, Qa = B.ec_mul(B.FP, G1, a), B.ec_mul(B.FP2, G2, a)
+    negG1 = B.ec_neg(B.FP, G1)
+    assert fe(mul(ml(G1, G2), ml(negG1, G2))) == one
+    assert fe(mul(mul(ml(Pa, G2), ml(negG1, Qa)), ml(G1, G2))) != one
+    assert fe(mul(mul(ml(Pa, G2), ml(negG1, Qa)), mul(ml(G1, G2), ml(negG1, G2)))) == one
+
+
 def validate(np_, prog, outs, phases, slot, nslots):
+    if isinstance(np_, str):
+        if not np_.startswith("NP"):
+            return  # checked in validate_split
+        np_ = int(np_[2:])
     B = _bls_points()
     rng = random.Random(1)
     one = [1] + [0] * 11
@@ -649,7 +716,7 @@ def emit(progs):
                 nops += 1
         ins = [slot[i] for i in prog.inputs]
         consts = [(slot[n], v) for v, n in prog.consts.items() if n in slot]
-        tag = "NP%d" % np_
+        tag = np_ if isinstance(np_, str) else "NP%d" % np_
         lines.append("// %s: %d phases (%d MUL, %d LIN, %d INV), %d ops, %d slots" % (
             tag, len(phases), sum(k == "mul" for k, _ in phases), sum(k == "lin" for k, _ in phases),
             sum(k == "inv" for k, _ in phases), nops, nslots))
@@ -669,17 +736,27 @@ def emit(progs):
     return "\n".join(lines)
 
 
-def main():
+TAGS = ("NP1", "NP2", "ML1", "MUL12", "FE")
+
+
+def build_all():
     progs = []
-    for np_ in (1, 2):
-        prog, outs = build(np_)
+    for tag in TAGS:
+        prog, outs = build_tag(tag)
         phases, live = schedule(prog, outs)
         slot, nslots = allocate(prog, outs, phases, live)
-        validate(np_, prog, outs, phases, slot, nslots)
+        validate(tag, prog, outs, phases, slot, nslots)
+        progs.append((tag, prog, outs, phases, slot, nslots))
+    validate_split(progs)
+    return progs
+
+
+def main():
+    progs = build_all()
+    for tag, prog, outs, phases, slot, nslots in progs:
         nm = sum(k == "mul" for k, _ in phases)
-        print("NP=%d: %d nodes, %d phases (%d MUL), %d slots, %d products" % (
-            np_, len(prog.nodes), len(phases), nm, nslots, sum(len(b) for k, b in phases if k == "mul")))
-        progs.append((np_, prog, outs, phases, slot, nslots))
+        print("%s: %d nodes, %d phases (%d MUL), %d slots, %d products" % (
+            tag, len(prog.nodes), len(phases), nm, nslots, sum(len(b) for k, b in phases if k == "mul")))
     out = os.path.join(HERE, "..", "csrc", "pairing_vm.hpp")
     open(out, "w").write(emit(progs))
 

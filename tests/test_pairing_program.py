@@ -11,12 +11,8 @@ sys.path.insert(0, os.path.join(ROOT, "drand_amd", "tools"))
 
 def test_pairing_program_valid_and_committed():
     import gen_pairing_vm as g
-    progs = []
-    for np_ in (1, 2):
-        prog, outs = g.build(np_)
-        phases, live = g.schedule(prog, outs)
-        slot, nslots = g.allocate(prog, outs, phases, live)
-        g.validate(np_, prog, outs, phases, slot, nslots)
+    progs = g.build_all()  # validates NP1 / NP2 on oracle points and ML1 x MUL12 x FE composed
+    for tag, prog, outs, phases, slot, nslots in progs:
         # invariants the device interpreter relies on
         assert nslots <= 400
         for kind, batch in phases:
@@ -28,7 +24,6 @@ def test_pairing_program_valid_and_committed():
                 n = prog.nodes[i]
                 assert len(n["a"]) <= g.MAXT and len(n.get("b", [])) <= g.MAXT
                 assert all(abs(c) <= g.MAXC for _, c in n["a"] + n.get("b", []))
-        progs.append((np_, prog, outs, phases, slot, nslots))
     text = g.emit(progs)
     with open(os.path.join(ROOT, "drand_amd", "csrc", "pairing_vm.hpp")) as f:
         assert f.read() == text, "csrc/pairing_vm.hpp is stale: rerun drand_amd/tools/gen_pairing_vm.py"
