@@ -72,52 +72,39 @@ DH_DEV fp fp_r2() {
   return r;
 }
 
+// Multi-limb carry chains use clang's __builtin_addc / __builtin_subc: they lower to one v_add_co / v_addc_co
+// (v_sub_co / v_subb_co) per limb with the carry in VCC or an SGPR pair. The uint64_t "t >> 32" / "t >> 63"
+// formulation compiled to 64-bit v_lshl_add_u64 + v_ashrrev + v_mov per limb (~140 VALU per fp_add, 48 now).
+
 // r = a - p if a >= p else a   (a < 2p)
 DH_DEV void fp_reduce_once(fp& a) {
   uint32_t d[12];
-  uint64_t borrow = 0;
+  unsigned br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)a.v[i] - p_limb(i) - borrow;
-    d[i] = (uint32_t)t;
-    borrow = (t >> 63) & 1;
-  }
-  // borrow == 0  <=>  a >= p
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(a.v[i], p_limb(i), br, &br);
+  // br == 0  <=>  a >= p
 #pragma unroll
-  for (int i = 0; i < 12; i++) a.v[i] = borrow ? a.v[i] : d[i];
+  for (int i = 0; i < 12; i++) a.v[i] = br ? a.v[i] : d[i];
 }
 
 DH_DEV fp fp_add(const fp& a, const fp& b) {
   fp r;
-  uint64_t c = 0;
+  unsigned c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)a.v[i] + b.v[i] + c;
-    r.v[i] = (uint32_t)t;
-    c = t >> 32;
-  }
+  for (int i = 0; i < 12; i++) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
   fp_reduce_once(r);  // a+b < 2p < 2^382, no limb overflow
   return r;
 }
 
 DH_DEV fp fp_sub(const fp& a, const fp& b) {
   fp r;
-  uint64_t borrow = 0;
+  unsigned br = 0, c = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)a.v[i] - b.v[i] - borrow;
-    r.v[i] = (uint32_t)t;
-    borrow = (t >> 63) & 1;
-  }
+  for (int i = 0; i < 12; i++) r.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
   // if negative add p back
-  uint32_t mask = 0u - (uint32_t)borrow;
-  uint64_t c = 0;
+  const uint32_t mask = 0u - br;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)r.v[i] + (p_limb(i) & mask) + c;
-    r.v[i] = (uint32_t)t;
-    c = t >> 32;
-  }
+  for (int i = 0; i < 12; i++) r.v[i] = __builtin_addc(r.v[i], p_limb(i) & mask, c, &c);
   return r;
 }
 
@@ -126,15 +113,11 @@ DH_DEV fp fp_neg(const fp& a) {
   uint32_t nz = 0;
 #pragma unroll
   for (int i = 0; i < 12; i++) nz |= a.v[i];
-  uint32_t mask = nz ? 0xffffffffu : 0u;
+  const uint32_t mask = nz ? 0xffffffffu : 0u;
   fp r;
-  uint64_t borrow = 0;
+  unsigned br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)(p_limb(i) & mask) - a.v[i] - borrow;
-    r.v[i] = (uint32_t)t;
-    borrow = (t >> 63) & 1;
-  }
+  for (int i = 0; i < 12; i++) r.v[i] = __builtin_subc(p_limb(i) & mask, a.v[i], br, &br);
   return r;
 }
 

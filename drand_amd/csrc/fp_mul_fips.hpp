@@ -12,6 +12,7 @@
 
 #include <utility>
 
+#include "fp_mac_g.hpp"
 #include "fp_mac_n.hpp"
 
 namespace dh {
@@ -144,22 +145,21 @@ __device__ __forceinline__ void mul_col(uint64_t& acc, uint32_t& hi, uint32_t m[
   constexpr uint32_t NP0 = 0xfffcfffdu;
   constexpr int LO = K > 11 ? K - 11 : 0, UP = K < 12 ? K : 11, MUP = K < 12 ? K - 1 : 11;
   constexpr int C = (UP - LO + 1) + (MUP >= LO ? MUP - LO + 1 : 0);
-  uint32_t xs[C], ys[C];
-  int c = 0;
+  constexpr int C1 = UP - LO + 1, C2 = C - C1;
+  uint32_t xs[C1], ys[C1], ms[C2 > 0 ? C2 : 1], ps[C2 > 0 ? C2 : 1];
 #pragma unroll
-  for (int i = LO; i <= UP; i++) { xs[c] = a[i]; ys[c] = b[K - i]; c++; }
+  for (int i = LO; i <= UP; i++) { xs[i - LO] = a[i]; ys[i - LO] = b[K - i]; }
 #pragma unroll
-  for (int i = LO; i <= MUP; i++) { xs[c] = m[i]; ys[c] = P[K - i]; c++; }
-  mac_n<C>(acc, hi, xs, ys);
+  for (int i = LO; i <= MUP; i++) { ms[i - LO] = m[i]; ps[i - LO] = P[K - i]; }
+  mac_g<C1, C2, 1>(acc, hi, xs, ys, ms, ps);  // the column's carry word starts here (hi not read)
   if constexpr (K < 12) {
     m[K] = (uint32_t)acc * NP0;
     uint32_t p0 = P[0];
-    mac_n<1>(acc, hi, &m[K], &p0);  // low word becomes 0
+    mac_g<0, 1, 0>(acc, hi, xs, ys, &m[K], &p0);  // low word becomes 0
   } else {
     r[K - 12] = (uint32_t)acc;
   }
   acc = (acc >> 32) | ((uint64_t)hi << 32);
-  hi = 0;
 }
 
 template <int K>
@@ -223,13 +223,9 @@ __device__ __forceinline__ void sqr_cols(std::integer_sequence<int, K...>, uint6
 __device__ __forceinline__ void fips_final_sub(uint32_t r[12], uint64_t acc, const uint32_t P[12]) {
   r[11] = (uint32_t)acc;  // < 2p < 2^382: no further carry
   uint32_t d[12];
-  uint64_t br = 0;
+  unsigned br = 0;  // one v_sub_co / v_subb_co per limb (see fp.hpp: fp_reduce_once)
 #pragma unroll
-  for (int i = 0; i < 12; i++) {
-    uint64_t t = (uint64_t)r[i] - P[i] - br;
-    d[i] = (uint32_t)t;
-    br = (t >> 63) & 1;
-  }
+  for (int i = 0; i < 12; i++) d[i] = __builtin_subc(r[i], P[i], br, &br);
 #pragma unroll
   for (int i = 0; i < 12; i++) r[i] = br ? r[i] : d[i];
 }
@@ -264,11 +260,12 @@ __device__ __forceinline__ void sqr_tri_col(uint64_t& acc, uint32_t& hi, uint32_
     uint32_t xs[D], ys[D];
 #pragma unroll
     for (int j = 0; j < D; j++) { xs[j] = a[LO + j]; ys[j] = a[K - LO - j]; }
-    mac_n<D>(acc, hi, xs, ys);
+    mac_g<D, 0, 1>(acc, hi, xs, ys, xs, ys);  // new carry word (hi not read)
+  } else {
+    hi = 0;
   }
   t[K] = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)hi << 32);
-  hi = 0;
 }
 
 // acc <- (hi:acc_hi) + w, i.e. shift the 96-bit column accumulator down one word and add the next input word
@@ -279,7 +276,6 @@ __device__ __forceinline__ void acc_shift_add(uint64_t& acc, uint32_t& hi, uint3
                : "+v"(lo), "+v"(h), "=&s"(c_)
                : "v"(w));
   acc = (uint64_t)lo | ((uint64_t)h << 32);
-  hi = 0;
 }
 
 template <int K>
@@ -293,22 +289,21 @@ __device__ __forceinline__ void sqr_red_col(uint64_t& acc, uint32_t& hi, uint32_
   uint32_t u = K == 0 ? t[0] << 1 : __builtin_amdgcn_alignbit(t[K], t[K > 0 ? K - 1 : 0], 31);
   if constexpr (K == 0) {
     acc = u;
-    hi = 0;
   } else {
     acc_shift_add(acc, hi, u);
   }
-  if constexpr (C > 0) {
-    uint32_t xs[C], ys[C];
-    int c = 0;
-    if constexpr ((K & 1) == 0) { xs[0] = a[K >> 1]; ys[0] = a[K >> 1]; c = 1; }
+  {
+    constexpr int C1 = C - CM;  // the diagonal square a_{K/2}^2 on even columns
+    uint32_t xs[1], ys[1], ms[CM > 0 ? CM : 1], ps[CM > 0 ? CM : 1];
+    if constexpr (C1) { xs[0] = a[K >> 1]; ys[0] = a[K >> 1]; }
 #pragma unroll
-    for (int j = 0; j < CM; j++) { xs[c + j] = m[LO + j]; ys[c + j] = P[K - LO - j]; }
-    mac_n<C>(acc, hi, xs, ys);
+    for (int j = 0; j < CM; j++) { ms[j] = m[LO + j]; ps[j] = P[K - LO - j]; }
+    mac_g<C1, CM, 1>(acc, hi, xs, ys, ms, ps);  // new carry word (hi not read; C = 0 sets it to 0)
   }
   if constexpr (K < 12) {
     m[K] = (uint32_t)acc * NP0;
     uint32_t p0 = P[0];
-    mac_n<1>(acc, hi, &m[K], &p0);
+    mac_g<0, 1, 0>(acc, hi, m, m, &m[K], &p0);
   } else {
     r[K - 12] = (uint32_t)acc;
   }
