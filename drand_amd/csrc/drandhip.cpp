@@ -267,7 +267,7 @@ dh::msm_geom geom_for(size_t gsize) {
   g.gsize = (uint32_t)gsize;
   g.c = c;
   g.nwin = (128 + c - 1) / c;
-  g.nbuck = 1u << c;
+  g.nbuck = (1u << (c - 1)) + 1;  // signed digits: |d| in [1, 2^(c-1)] (k_msm.hip: signed_digit)
   uint32_t nseg = std::max(1u, std::min(2048u, g.nbuck / 32));
   g.nseg = nseg;
   g.seglen = (g.nbuck - 1 + nseg - 1) / nseg;
@@ -378,7 +378,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     return fail(DH_EINVAL, "bad previous-signature stride %zu", prev_stride);
   if (stats) memset(stats, 0, 4 * sizeof(uint64_t));
   if (n == 0) return DH_OK;
-  if (n > 0xffffffffu) return fail(DH_EINVAL, "batch too large");
+  if (n >= 0x80000000u) return fail(DH_EINVAL, "batch too large");  // sorted-list entries keep a sign bit
   const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
   const size_t aw = jw * 2 / 3;
 

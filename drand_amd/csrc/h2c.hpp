@@ -102,34 +102,36 @@ DH_DEV jac<fp> iso11_jac(const jac<fp>& p) {
   return r;
 }
 
-// SSWU output (x = xn / xd, y affine) as a Jacobian point of E1': Z = xd, X = xn xd, Y = y xd^3
-DH_DEV jac<fp> swu_jac(const swu_out<fp>& s) {
-  jac<fp> r;
+// SSWU output (x = xn / xd, y affine) as a Jacobian point of E': Z = xd, X = xn xd, Y = y xd^3
+template <class F>
+DH_DEV jac<F> swu_jac(const swu_out<F>& s) {
+  jac<F> r;
   r.z = s.xd;
-  r.x = fp_mul(s.xn, s.xd);
-  r.y = fp_mul(s.y, fp_mul(fp_sqr(s.xd), s.xd));
+  r.x = f_mul(s.xn, s.xd);
+  r.y = f_mul(s.y, f_mul(f_sqr(s.xd), s.xd));
   return r;
 }
 
 // add-2007-bl on Jacobian points (the addition law does not involve the curve's a, so it holds on E1' with
 // A' != 0). Returns false, leaving r unset, when x0 == x1 (P == Q or P == -Q): the caller takes the
 // exceptional path. Neither input may be the identity (SSWU outputs never are: xd = tv4 != 0).
-DH_DEV bool jac_add_distinct(jac<fp>& r, const jac<fp>& p, const jac<fp>& q) {
-  fp z1z1 = fp_sqr(p.z);
-  fp z2z2 = fp_sqr(q.z);
-  fp u1 = fp_mul(p.x, z2z2);
-  fp u2 = fp_mul(q.x, z1z1);
-  fp s1 = fp_mul(fp_mul(p.y, q.z), z2z2);
-  fp s2 = fp_mul(fp_mul(q.y, p.z), z1z1);
-  fp h = fp_sub(u2, u1);
-  if (fp_is_zero(h)) return false;
-  fp rr = fp_dbl(fp_sub(s2, s1));
-  fp i = fp_sqr(fp_dbl(h));
-  fp j = fp_mul(h, i);
-  fp v = fp_mul(u1, i);
-  r.x = fp_sub(fp_sub(fp_sqr(rr), j), fp_dbl(v));
-  r.y = fp_sub(fp_mul(rr, fp_sub(v, r.x)), fp_dbl(fp_mul(s1, j)));
-  r.z = fp_mul(fp_sub(fp_sub(fp_sqr(fp_add(p.z, q.z)), z1z1), z2z2), h);
+template <class F>
+DH_DEV bool jac_add_distinct(jac<F>& r, const jac<F>& p, const jac<F>& q) {
+  F z1z1 = f_sqr(p.z);
+  F z2z2 = f_sqr(q.z);
+  F u1 = f_mul(p.x, z2z2);
+  F u2 = f_mul(q.x, z1z1);
+  F s1 = f_mul(f_mul(p.y, q.z), z2z2);
+  F s2 = f_mul(f_mul(q.y, p.z), z1z1);
+  F h = f_sub(u2, u1);
+  if (f_is_zero(h)) return false;
+  F rr = f_dbl(f_sub(s2, s1));
+  F i = f_sqr(f_dbl(h));
+  F j = f_mul(h, i);
+  F v = f_mul(u1, i);
+  r.x = f_sub(f_sub(f_sqr(rr), j), f_dbl(v));
+  r.y = f_sub(f_mul(rr, f_sub(v, r.x)), f_dbl(f_mul(s1, j)));
+  r.z = f_mul(f_sub(f_sub(f_sqr(f_add(p.z, q.z)), z1z1), z2z2), h);
   return true;
 }
 
@@ -176,38 +178,44 @@ DH_DEV swu_out<fp2> sswu_g2(const fp2& u) {
   return {x, tv4, y};
 }
 
-// 3-isogeny E2' -> E2 (RFC 9380 E.3), same homogeneous evaluation as iso11
-DH_DEV jac<fp2> iso3(const swu_out<fp2>& s) {
+// 3-isogeny E2' -> E2 (RFC 9380 E.3) on a Jacobian point of E2', same homogeneous evaluation as iso11_jac
+DH_DEV jac<fp2> iso3_jac(const jac<fp2>& p) {
   using namespace cst;
+  const fp2 D = fp2_sqr(p.z);
   fp2 xn = fp2_c(ISO3_XNUM[ISO3_XNUM_LEN - 1]);
   fp2 xd = fp2_c(ISO3_XDEN[ISO3_XDEN_LEN - 1]);
   fp2 yn = fp2_c(ISO3_YNUM[ISO3_YNUM_LEN - 1]);
   fp2 yd = fp2_c(ISO3_YDEN[ISO3_YDEN_LEN - 1]);
-  fp2 zp = s.xd;
+  fp2 zp = D;
 #pragma unroll 1
   for (int j = 1; j < ISO3_YNUM_LEN; j++) {
-    if (j > 1) zp = fp2_mul(zp, s.xd);
-    yn = fp2_add(fp2_mul(yn, s.xn), fp2_mul(fp2_c(ISO3_YNUM[ISO3_YNUM_LEN - 1 - j]), zp));
-    yd = fp2_add(fp2_mul(yd, s.xn), fp2_mul(fp2_c(ISO3_YDEN[ISO3_YDEN_LEN - 1 - j]), zp));
-    if (j < ISO3_XNUM_LEN) xn = fp2_add(fp2_mul(xn, s.xn), fp2_mul(fp2_c(ISO3_XNUM[ISO3_XNUM_LEN - 1 - j]), zp));
-    if (j < ISO3_XDEN_LEN) xd = fp2_add(fp2_mul(xd, s.xn), fp2_mul(fp2_c(ISO3_XDEN[ISO3_XDEN_LEN - 1 - j]), zp));
+    if (j > 1) zp = fp2_mul(zp, D);
+    yn = fp2_add(fp2_mul(yn, p.x), fp2_mul(fp2_c(ISO3_YNUM[ISO3_YNUM_LEN - 1 - j]), zp));
+    yd = fp2_add(fp2_mul(yd, p.x), fp2_mul(fp2_c(ISO3_YDEN[ISO3_YDEN_LEN - 1 - j]), zp));
+    if (j < ISO3_XNUM_LEN) xn = fp2_add(fp2_mul(xn, p.x), fp2_mul(fp2_c(ISO3_XNUM[ISO3_XNUM_LEN - 1 - j]), zp));
+    if (j < ISO3_XDEN_LEN) xd = fp2_add(fp2_mul(xd, p.x), fp2_mul(fp2_c(ISO3_XDEN[ISO3_XDEN_LEN - 1 - j]), zp));
   }
-  fp2 a = fp2_mul(xd, s.xd);
+  const fp2 a = fp2_mul(xd, D);
+  const fp2 z3 = fp2_mul(D, p.z);
+  const fp2 ydz3 = fp2_mul(yd, z3);
   jac<fp2> r;
-  r.z = fp2_mul(a, yd);
-  r.x = fp2_mul(fp2_mul(xn, yd), r.z);
-  r.y = fp2_mul(fp2_mul(fp2_mul(s.y, yn), a), fp2_sqr(r.z));
+  r.z = fp2_mul(a, ydz3);
+  r.x = fp2_mul(fp2_mul(xn, ydz3), r.z);
+  r.y = fp2_mul(fp2_mul(fp2_mul(p.y, yn), a), fp2_sqr(r.z));
   return r;
 }
 
+// hash_to_curve(G2) without clear_cofactor, one isogeny after the addition on E2' (see h2c_g1_noclear)
 DH_DEV jac<fp2> h2c_g2_noclear(const sha_h& digest, int dst_id) {
   uint32_t b[8][8];
   xmd32<8>(b, digest, dst_id);
   fp2 u0 = {fp_from_be512(b[0], b[1]), fp_from_be512(b[2], b[3])};
   fp2 u1 = {fp_from_be512(b[4], b[5]), fp_from_be512(b[6], b[7])};
-  jac<fp2> q0 = iso3(sswu_g2(u0));
-  jac<fp2> q1 = iso3(sswu_g2(u1));
-  return jac_add(q0, q1);
+  const jac<fp2> p0 = swu_jac(sswu_g2(u0));
+  const jac<fp2> p1 = swu_jac(sswu_g2(u1));
+  jac<fp2> s;
+  if (jac_add_distinct(s, p0, p1)) return iso3_jac(s);
+  return jac_add(iso3_jac(p0), iso3_jac(p1));
 }
 
 // psi (untwist-Frobenius-twist) on E2 and its square, Jacobian

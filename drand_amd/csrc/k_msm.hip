@@ -14,8 +14,25 @@ DH_DEV uint32_t scalar_digit(const uint4& s, int bit, int c) {
   return (uint32_t)v & ((1u << c) - 1);
 }
 
+// Signed window digits (scalars < 2^127, k_scalars): window w holds d_w = v_w + carry_w, mapped to
+// [-2^(c-1), 2^(c-1)) with a carry into the next window; the top window needs no mapping (nwin * c >= 128
+// leaves it at least one spare bit, so its digit is at most 2^(c-1)). Bucket |d| in [1, 2^(c-1)], the sign
+// travels in bit 31 of the sorted-list entry and the bucket pass negates the point: half the buckets of
+// unsigned digits, so half the bucket-reduction work, for the same accumulation count.
+constexpr uint32_t NEG_BIT = 0x80000000u;
+DH_DEV int32_t signed_digit(const uint4& s, int w, const msm_geom& g, uint32_t& carry) {
+  const uint32_t v = scalar_digit(s, w * g.c, g.c) + carry;
+  const uint32_t half = 1u << (g.c - 1);
+  if (w + 1 < g.nwin && v >= half) {
+    carry = 1;
+    return (int32_t)v - (int32_t)(1u << g.c);
+  }
+  carry = 0;
+  return (int32_t)v;
+}
+
 // Entry e refers to point pidx[e] with scalar scal[sidx ? sidx[e] : pidx[e]] and belongs to group
-// grp ? grp[e] : e / gsize. The sorted list stores point indices, bucket by bucket.
+// grp ? grp[e] : e / gsize. The sorted list stores point indices (| NEG_BIT for a negative digit), bucket by bucket.
 DH_DEV size_t entry_group(const uint32_t* grp, size_t e, uint32_t gsize) { return grp ? grp[e] : e / gsize; }
 
 __global__ void k_msm_hist(const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ sidx,
@@ -25,9 +42,10 @@ __global__ void k_msm_hist(const uint32_t* __restrict__ pidx, const uint32_t* __
   if (e >= m) return;
   const uint4 s = scal[sidx ? sidx[e] : pidx[e]];
   const size_t gi = entry_group(grp, e, g.gsize);
+  uint32_t carry = 0;
   for (int w = 0; w < g.nwin; w++) {
-    uint32_t d = scalar_digit(s, w * g.c, g.c);
-    if (d) atomicAdd(&cnt[(gi * g.nwin + w) * g.nbuck + d], 1u);
+    const int32_t d = signed_digit(s, w, g, carry);
+    if (d) atomicAdd(&cnt[(gi * g.nwin + w) * g.nbuck + (uint32_t)(d < 0 ? -d : d)], 1u);
   }
 }
 
@@ -39,11 +57,12 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ pidx, const uint32_t*
   const uint32_t idx = pidx[e];
   const uint4 s = scal[sidx ? sidx[e] : idx];
   const size_t gi = entry_group(grp, e, g.gsize);
+  uint32_t carry = 0;
   for (int w = 0; w < g.nwin; w++) {
-    uint32_t d = scalar_digit(s, w * g.c, g.c);
+    const int32_t d = signed_digit(s, w, g, carry);
     if (d) {
-      uint32_t pos = atomicAdd(&cursor[(gi * g.nwin + w) * g.nbuck + d], 1u);
-      list[pos] = idx;
+      uint32_t pos = atomicAdd(&cursor[(gi * g.nwin + w) * g.nbuck + (uint32_t)(d < 0 ? -d : d)], 1u);
+      list[pos] = d < 0 ? (idx | NEG_BIT) : idx;
     }
   }
 }
@@ -153,11 +172,17 @@ __global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket(const uint32_t* _
   uint32_t head_kind = 0, tail_key = NO_KEY;
   jac<F> acc = jac_inf<F>();
   for (uint32_t j = (uint32_t)s; j < e; j++) {
-    const uint32_t idx = list[j];
+    const uint32_t raw = list[j];
+    const uint32_t idx = raw & ~NEG_BIT;
+    const bool neg = (raw & NEG_BIT) != 0;
     if constexpr (AFFINE) {
-      acc = jac_add_aff(acc, ld_aff_aos<F>(pts, idx));
+      aff<F> pt = ld_aff_aos<F>(pts, idx);
+      pt.y = f_select(neg, f_neg(pt.y), pt.y);
+      acc = jac_add_aff(acc, pt);
     } else {
-      acc = jac_add(acc, ld_jac_aos<F>(pts, idx));
+      jac<F> pt = ld_jac_aos<F>(pts, idx);
+      pt.y = f_select(neg, f_neg(pt.y), pt.y);
+      acc = jac_add(acc, pt);
     }
     const bool ends = j + 1 == kend;
     if (ends || j + 1 == e) {

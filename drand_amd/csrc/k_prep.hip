@@ -96,7 +96,9 @@ __global__ __launch_bounds__(256) void k_scalars(const uint32_t* __restrict__ se
   w[15] = 40 * 8;
   sha_h s = sha_iv();
   sha_compress(s, w);
-  uint4 r = make_uint4(s.h[3], s.h[2], s.h[1], s.h[0]);  // little-endian words of a 128-bit integer
+  // little-endian words of a 127-bit integer (top bit cleared: the MSM's signed window digits need one spare
+  // bit; the batch check's soundness error is 2^-127 per group)
+  uint4 r = make_uint4(s.h[3], s.h[2], s.h[1], s.h[0] & 0x7fffffffu);
   if (status[i] != DEC_OK) r = make_uint4(0, 0, 0, 0);
   scal[i] = r;
 }

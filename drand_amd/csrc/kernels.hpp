@@ -7,7 +7,8 @@
 namespace dh {
 
 // Pippenger geometry for one MSM level: entries are cut into groups of `gsize` consecutive entries;
-// each group has nwin windows of c bits (128-bit scalars) with nbuck = 2^c buckets (digit 0 unused);
+// each group has nwin windows of c bits (127-bit scalars, signed digits) with nbuck = 2^(c-1) + 1 buckets
+// (index = |digit|, 0 unused);
 // bucket reduction splits the digits of a window into nseg segments of seglen digits.
 struct msm_geom {
   uint32_t gsize;
