@@ -15,6 +15,9 @@ namespace dh {
 
 // ---- overload set so the point code below is written once for fp and fp2
 DH_DEV fp f_add(const fp& a, const fp& b) { return fp_add(a, b); }
+// sum that only feeds a product: unreduced (< 2p) over Fp, where the product is one Montgomery multiplication;
+// reduced over Fp2, whose product adds and subtracts its operands' coordinates first (they must be < p there)
+DH_DEV fp f_add_nr(const fp& a, const fp& b) { return fp_add_nr(a, b); }
 DH_DEV fp f_sub(const fp& a, const fp& b) { return fp_sub(a, b); }
 DH_DEV fp f_dbl(const fp& a) { return fp_dbl(a); }
 DH_DEV fp f_neg(const fp& a) { return fp_neg(a); }
@@ -28,6 +31,7 @@ DH_DEV void f_set_one(fp& a) { a = fp_one(); }
 DH_DEV fp f_inv(const fp& a) { return fp_inv(a); }
 
 DH_DEV fp2 f_add(const fp2& a, const fp2& b) { return fp2_add(a, b); }
+DH_DEV fp2 f_add_nr(const fp2& a, const fp2& b) { return fp2_add(a, b); }
 DH_DEV fp2 f_sub(const fp2& a, const fp2& b) { return fp2_sub(a, b); }
 DH_DEV fp2 f_dbl(const fp2& a) { return fp2_dbl(a); }
 DH_DEV fp2 f_neg(const fp2& a) { return fp2_neg(a); }
@@ -80,9 +84,9 @@ DH_DEV jac<F> jac_dbl(const jac<F>& p) {
   F a = f_sqr(p.x);
   F b = f_sqr(p.y);
   F c = f_sqr(b);
-  F d = f_sub(f_sub(f_sqr(f_add(p.x, b)), a), c);
+  F d = f_sub(f_sub(f_sqr(f_add_nr(p.x, b)), a), c);
   d = f_dbl(d);
-  F e = f_add(f_dbl(a), a);
+  F e = f_add_nr(f_dbl(a), a);  // 3a < 2p: only ever a product operand below
   F f = f_sqr(e);
   jac<F> r;
   r.x = f_sub(f, f_dbl(d));

@@ -96,6 +96,17 @@ DH_DEV fp fp_add(const fp& a, const fp& b) {
   return r;
 }
 
+// a + b WITHOUT the reduction, for operands that only feed a Montgomery product: a, b < p gives a sum < 2p, and
+// the product (fp_mul_fips.hpp) is exact and fully reduced for inputs < 2p because 4p < R = 2^384
+// (t = (xy + mp) / R < 4p^2/R + p < 2p before its one conditional subtraction).
+DH_DEV fp fp_add_nr(const fp& a, const fp& b) {
+  fp r;
+  unsigned c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+  return r;
+}
+
 DH_DEV fp fp_sub(const fp& a, const fp& b) {
   fp r;
   unsigned br = 0, c = 0;

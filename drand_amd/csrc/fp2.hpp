@@ -23,16 +23,17 @@ DH_DEV fp2 fp2_conj(const fp2& a) { return {a.c0, fp_neg(a.c1)}; }
 DH_DEV fp2 fp2_mul(const fp2& a, const fp2& b) {
   fp t0 = fp_mul(a.c0, b.c0);
   fp t1 = fp_mul(a.c1, b.c1);
-  fp t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  fp t2 = fp_mul(fp_add_nr(a.c0, a.c1), fp_add_nr(b.c0, b.c1));  // unreduced sums < 2p feed the product
   return {fp_sub(t0, t1), fp_sub(fp_sub(t2, t0), t1)};
 }
 
-// complex squaring: 2 Fp products
+// complex squaring: 2 Fp products (operand coordinates must be canonical, < p: they are added / subtracted here)
 DH_DEV fp2 fp2_sqr(const fp2& a) {
-  fp t0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
-  fp t1 = fp_mul(a.c0, a.c1);
-  return {t0, fp_dbl(t1)};
+  fp t0 = fp_mul(fp_add_nr(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  fp t1 = fp_mul(fp_add_nr(a.c0, a.c0), a.c1);  // 2 a0 a1 with the doubling folded into the operand
+  return {t0, t1};
 }
+
 
 DH_DEV fp2 fp2_mul_fp(const fp2& a, const fp& b) { return {fp_mul(a.c0, b), fp_mul(a.c1, b)}; }
 
