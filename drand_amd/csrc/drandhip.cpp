@@ -263,6 +263,14 @@ dh::msm_geom geom_for(size_t gsize) {
   int lg = 0;
   while (((size_t)1 << (lg + 1)) <= gsize) lg++;
   int c = std::max(3, std::min(16, lg - 2));
+  // 127-bit scalars: keep the top window's t bits at >= c - 4, since each of its 2^(t-1) buckets collects
+  // ~m / 2^(t-1) entries and a bucket that spans many chunks is summed serially by k_msm_bucket_fix
+  // (c = 14 would leave t = 1: two buckets holding the whole set). Allowed: 16, 13, 10, 8, 5, 4, 3.
+  while (c > 3) {
+    const int nw = (128 + c - 1) / c, t = 127 - c * (nw - 1);
+    if (t >= c - 4) break;
+    c--;
+  }
   dh::msm_geom g;
   g.gsize = (uint32_t)gsize;
   g.c = c;
