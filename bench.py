@@ -33,15 +33,15 @@ sys.path.insert(0, ROOT)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--rounds", type=int, default=1 << 20, help="rounds per GPU per step")
     ap.add_argument("--scheme", default="bls-unchained-g1-rfc9380")
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-steps", type=int, default=2, help="single-stream batches timed for the roofline")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=6,
                     help="batches in flight per GPU (host threads, each with its own HIP stream in libdrandhip)")
     return ap.parse_args()
 
@@ -148,7 +148,10 @@ def main():
         lib.dh_profile_read(buf, len(buf))
         return json.loads(buf.value.decode())
 
-    run_steps(max(args.warmup, 1) if args.warmup else 0, S)
+    # warm-up: at least one batch per stream, so every library worker (stream + device workspace) exists before
+    # the timed region; W < S would leave workspace allocation inside it
+    warm_batches = max(args.warmup, S) if args.warmup else 0
+    run_steps(warm_batches, S)
     lib.dh_profile(1)
     if world > 1:
         dist.barrier()
@@ -219,7 +222,7 @@ def main():
         "roofline": roof,
         "node_roofline_frac": round(value * w_beacon / (peak * world), 4),
         "verdicts_ok": ok,
-        "streams": S,
+        "streams": S, "warmup_batches": warm_batches,
         "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in prof.items()},
         "stages_ms_single_stream": {k: round(v["total_ms"] / max(1, v["count"]), 3) for k, v in prof1.items()},
         "sign_seconds": round(t_sign, 2),
