@@ -123,6 +123,36 @@ def test_large_batch_with_corruption(dh, scheme, oracle):
         assert rand2[i].tobytes() == hashlib.sha256(sigs2[i].tobytes()).digest()
 
 
+def test_dense_corruption_every_window_geometry(dh):
+    """131 195 quicknet rounds (level 0 at c = 13, whose top window must stay populated) with 0.5% corrupted
+    rounds in three classes, then a small batch where EVERY round is bad: the signed-digit MSM runs at every
+    bisection geometry (c = 13, 10, 5, 3) and the rejected set is exactly the corrupted one."""
+    s = dh.scheme_from_name("bls-unchained-g1-rfc9380")
+    sk = hashlib.sha256(b"dense").digest()
+    n = (1 << 17) + 123
+    rounds = np.arange(7, n + 7, dtype=np.uint64)
+    sigs = s.sign_beacons(sk, rounds)
+    pk = s.public_key(sk)
+    rng = np.random.default_rng(777)
+    bad = np.sort(rng.choice(n, size=n // 200, replace=False))
+    sigs2 = sigs.copy()
+    for k, i in enumerate(bad):
+        if k % 3 == 0:
+            sigs2[i] = sigs[(i + 5) % n]
+        elif k % 3 == 1:
+            sigs2[i, 17] ^= 0x10
+        else:
+            sigs2[i, 0] ^= 0x20
+    v, rand = s.verify_beacons(pk, rounds, sigs2, seed=11)
+    assert np.flatnonzero(~v).tolist() == bad.tolist()
+    for i in [0, int(bad[0]), n - 1]:
+        assert rand[i].tobytes() == hashlib.sha256(sigs2[i].tobytes()).digest()
+    m = 300
+    sigs3 = np.ascontiguousarray(np.roll(sigs[:m], 1, axis=0))  # every signature belongs to another round
+    v3, _ = s.verify_beacons(pk, rounds[:m], sigs3, seed=12)
+    assert not v3.any()
+
+
 def test_seed_independence(dh):
     c = json.load(open(os.path.join(GOLD, "negatives.json")))["bls-unchained-g1-rfc9380"]
     s = dh.scheme_from_name("bls-unchained-g1-rfc9380")
