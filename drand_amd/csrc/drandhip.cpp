@@ -18,6 +18,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <mutex>
 #include <string>
@@ -373,6 +374,63 @@ static hipError_t leaf_check(worker* w, bool g2, const uint32_t* entries, size_t
                                   w->vm_live.as<uint8_t>(), w->vm_done.as<uint8_t>(), verdict, st);
 }
 
+// Bisection ladder. DRANDHIP_BISECT="4096,256,16,2" fixes the group sizes after level 0 (tests, experiments);
+// otherwise next_group_size picks each level from the failure rate the previous level observed.
+static const std::vector<size_t>& fixed_ladder() {
+  static const std::vector<size_t> v = [] {
+    std::vector<size_t> r;
+    const char* e = getenv("DRANDHIP_BISECT");
+    while (e && *e) {
+      char* end = nullptr;
+      unsigned long x = strtoul(e, &end, 10);
+      if (end == e) break;
+      if (x >= 2) r.push_back(x);
+      e = *end ? end + 1 : end;
+    }
+    return r;
+  }();
+  return v;
+}
+
+// Expected-cost choice of the next bisection level (group size; 1 = per-round leaf checks). Level costs
+// fitted to the chained-replay sweep on one MI355X (bench/bisect_sweep.sh, ms at 1M G2 rounds): an MSM over m
+// rounds costs ~9 + 1.8e-6 m nwin(g), a group-check launch ~12 + 0.0025 groups (the pairing program's
+// latency floor), per-round leaf checks ~12 + 0.005 m. Faults are modelled as Poisson at the density the last
+// level observed (faulty groups -> -ln(1 - f) faults per group, at least one per failing group; when every
+// group failed, 5 per group). The next size minimises the expected cost of the rest of the descent.
+static double msm_cost_ms(double m, size_t g) { return 9.0 + 1.8e-6 * m * (double)geom_for(g).nwin; }
+static double check_cost_ms(double groups) { return 12.0 + 0.0025 * groups; }
+static double leaf_cost_ms(double m) { return 12.0 + 0.005 * m; }
+
+static double descent_cost(double m, double d, size_t gprev, size_t* best) {
+  double c_best = leaf_cost_ms(m);
+  if (best) *best = 1;
+  for (size_t g = 4; g < gprev && (double)g < m; g *= 4) {
+    const double q = -std::expm1(-d * (double)g);  // P(group of g holds a fault)
+    const double m_next = m * q;
+    const double c = msm_cost_ms(m, g) + check_cost_ms(m / (double)g) +
+                     (m_next < 1.0 ? 0.0 : descent_cost(m_next, d / std::max(q, 1e-12), g, nullptr));
+    if (c < c_best) {
+      c_best = c;
+      if (best) *best = g;
+    }
+  }
+  return c_best;
+}
+
+static size_t next_group_size(size_t gsize, size_t ngroups, size_t nfail, size_t m_prev, size_t m_next) {
+  // level 0 (one group) says only that some round is bad: 1024 costs about what 4096 does over 1M rounds and
+  // its groups still pass at a 0.1% fault density (4096-round groups then all fail)
+  if (gsize == m_prev && m_prev > 4096) return 1024;
+  const double f = (double)nfail / (double)ngroups;
+  const double per_group = nfail == ngroups ? 5.0 : -std::log1p(-f);
+  const double faults = std::max((double)nfail, per_group * (double)ngroups);
+  const double density = std::min(1.0, faults / (double)std::max<size_t>(m_next, 1));
+  size_t g = 1;
+  descent_cost((double)m_next, density, gsize, &g);
+  return g;
+}
+
 // core pipeline on device-resident inputs
 int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                 size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
@@ -446,12 +504,16 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   // bisection levels: group sizes n, 4096, 256, 16, 2, then per-round leaves (a failing group is re-checked
   // as smaller groups with the same scalars; only rounds of failing pairs reach a per-round pairing check)
   size_t m = n;
-  std::vector<size_t> sizes = {n};
-  for (size_t gs : {4096, 256, 16, 2})
-    if (n > gs) sizes.push_back(gs);
+  static const char* const msm_names[8] = {"msm_level0", "msm_bisect1", "msm_bisect2", "msm_bisect3",
+                                           "msm_bisect4", "msm_bisect5", "msm_bisect6", "msm_bisect7+"};
+  static const char* const chk_names[8] = {"k_group_check_level0", "k_group_check_bisect1", "k_group_check_bisect2",
+                                           "k_group_check_bisect3", "k_group_check_bisect4", "k_group_check_bisect5",
+                                           "k_group_check_bisect6", "k_group_check_bisect7+"};
+  const std::vector<size_t>& fixed = fixed_ladder();
+  size_t gsize = n;
   int level = 0;
-  for (size_t li = 0; li < sizes.size() && m > 0; li++) {
-    const size_t gsize = std::min(sizes[li], m);
+  while (m > 0 && gsize > 1) {
+    gsize = std::min(gsize, m);
     const dh::msm_geom g = geom_for(gsize);
     const size_t ngroups = (m + gsize - 1) / gsize;
     const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
@@ -470,11 +532,11 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
                   w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>(), w->part.as<uint32_t>(),
                   w->meta.as<uint32_t>(), 0};
-    HIP_TRY(T.run(level == 0 ? "msm_level0" : "msm_bisect", [&] {
+    HIP_TRY(T.run(msm_names[std::min(level, 7)], [&] {
       return dh::launch_msm(g2, g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(), w->sig_aff.as<uint32_t>(),
                             w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st);
     }));
-    HIP_TRY(T.run(level == 0 ? "k_group_check_level0" : "k_group_check_bisect", [&] {
+    HIP_TRY(T.run(chk_names[std::min(level, 7)], [&] {
       return group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups, w->key_aff.as<uint32_t>(),
                          w->pass.as<uint8_t>(), st);
     }));
@@ -499,8 +561,11 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     for (size_t gi = 0; gi < ngroups; gi++)
       if (!w->h_pass[gi])
         for (size_t e = gi * gsize; e < std::min(m, (gi + 1) * gsize); e++) w->h_next.push_back(w->h_entries[e]);
+    const size_t m_prev = m;
     m = w->h_next.size();
     HIP_TRY(hipMemcpyAsync(w->entries.p, w->h_next.data(), m * 4, hipMemcpyHostToDevice, st));
+    gsize = fixed.empty() ? next_group_size(gsize, ngroups, nfail, m_prev, m)
+                          : (size_t)(level - 1 < (int)fixed.size() ? fixed[level - 1] : 1);
   }
   if (m > 0) {
     HIP_TRY(T.run("k_leaf_check", [&] {

@@ -96,7 +96,7 @@ def test_device_signer_matches_oracle(dh, scheme, oracle):
 @pytest.mark.parametrize("scheme", ["bls-unchained-g1-rfc9380", "pedersen-bls-unchained"])
 def test_large_batch_with_corruption(dh, scheme, oracle):
     """n rounds signed on the device, a seeded set corrupted: exactly those rounds are rejected; the
-    bisection levels (group sizes n, 4096, 64, leaves) run. Corrupted rows are cross-checked on the oracle."""
+    bisection levels the expected-cost ladder picks run. Corrupted rows are cross-checked on the oracle."""
     n = 20000 if scheme == "bls-unchained-g1-rfc9380" else 6000
     s = dh.scheme_from_name(scheme)
     sk = hashlib.sha256(b"large-" + scheme.encode()).digest()
@@ -126,7 +126,8 @@ def test_large_batch_with_corruption(dh, scheme, oracle):
 def test_dense_corruption_every_window_geometry(dh):
     """131 195 quicknet rounds (level 0 at c = 13, whose top window must stay populated) with 0.5% corrupted
     rounds in three classes, then a small batch where EVERY round is bad: the signed-digit MSM runs at every
-    bisection geometry (c = 13, 10, 5, 3) and the rejected set is exactly the corrupted one."""
+    window geometry the expected-cost ladder picks (c = 13 at level 0, 8 for 1024-round groups, 5/4/3 for
+    the small ones) and the rejected set is exactly the corrupted one."""
     s = dh.scheme_from_name("bls-unchained-g1-rfc9380")
     sk = hashlib.sha256(b"dense").digest()
     n = (1 << 17) + 123
@@ -324,3 +325,18 @@ def test_one_lane_pairing_path(dh):
     neg = json.load(open(os.path.join(GOLD, "negatives.json")))
     for name, v in got.items():
         assert v == [x["valid"] for x in neg[name]["cases"]], name
+
+
+@pytest.mark.parametrize("ladder", ["4096,256,16,2", "64"])
+def test_fixed_bisection_ladder(dh, ladder):
+    """The bisection is exact whatever the group sizes: a fixed ladder (DRANDHIP_BISECT, the r01 sizes with the
+    c = 10 window geometry, and a single level of 64 before leaves) rejects exactly the corrupted rounds, as the
+    default expected-cost ladder does in the tests above."""
+    import subprocess
+    import sys
+    env = dict(os.environ, DRANDHIP_BISECT=ladder)
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "fixed_ladder_check.py")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert got["rejected"] == got["expected"] and len(got["expected"]) == 200
