@@ -109,11 +109,10 @@ def main():
     torch.cuda.synchronize()
 
     def verify(slot):
-        stats = (ctypes.c_uint64 * 4)()
         rc = lib.dh_verify_batch_device(sch.id, pk, len(pk), ctypes.c_void_p(d_rounds.data_ptr()),
                                         ctypes.c_void_p(d_sigs.data_ptr()), sch.sig_len, None, 0, None, n,
                                         ctypes.c_void_p(d_verdict[slot].data_ptr()),
-                                        ctypes.c_void_p(d_rand[slot].data_ptr()), 0, None, stats)
+                                        ctypes.c_void_p(d_rand[slot].data_ptr()), 0, None, None)
         if rc != 0:
             raise RuntimeError("dh_verify_batch_device: %s" % _lib.last_error())
 

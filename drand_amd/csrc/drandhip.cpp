@@ -95,6 +95,7 @@ struct worker {
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
       r_sigbytes, r_status2, r_aff2, r_entries2;
   std::vector<uint8_t> h_pass;
+  std::vector<uint8_t> h_verdict;
   // decoded group key cache: the same key is used for every batch of a chain
   uint8_t cached_key[96];
   size_t cached_key_len = 0;
@@ -574,8 +575,17 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     }));
     if (stats) stats[2] = m;
   }
+  if (stats) {  // rejected = decode/subgroup failures + failed leaves (1 MB D2H per 1M rounds, only when asked)
+    w->h_verdict.resize(n);
+    HIP_TRY(hipMemcpyAsync(w->h_verdict.data(), d_verdict, n, hipMemcpyDeviceToHost, st));
+  }
   HIP_TRY(hipStreamSynchronize(st));
-  if (stats) stats[0] = (uint64_t)level;
+  if (stats) {
+    stats[0] = (uint64_t)level;
+    size_t ok = 0;
+    for (uint8_t v : w->h_verdict) ok += v ? 1 : 0;
+    stats[3] = n - ok;
+  }
   return DH_OK;
 }
 

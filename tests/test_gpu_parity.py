@@ -340,3 +340,37 @@ def test_fixed_bisection_ladder(dh, ladder):
     assert r.returncode == 0, r.stderr[-2000:]
     got = json.loads(r.stdout.strip().splitlines()[-1])
     assert got["rejected"] == got["expected"] and len(got["expected"]) == 200
+
+
+def test_device_entry_stats(dh):
+    """dh_verify_batch_device on HBM-resident inputs fills stats_out = {levels, groups_failed, leaf_rounds,
+    rounds_rejected} (include/drandhip.h): rounds_rejected counts decode failures and failed leaves alike."""
+    import ctypes
+    import torch
+    from drand_amd import _lib
+    lib = _lib.load()
+    s = dh.scheme_from_name("bls-unchained-g1-rfc9380")
+    sk = hashlib.sha256(b"stats").digest()
+    n = 5000
+    rounds = np.arange(1, n + 1, dtype=np.uint64)
+    sigs = s.sign_beacons(sk, rounds)
+    pk = s.public_key(sk)
+    sigs[10] = sigs[11]          # valid point, wrong round: fails its group, then its leaf
+    sigs[4000, 0] ^= 0x20        # negated point: also a leaf failure
+    sigs[2500, 5] ^= 0x01        # usually off the curve: rejected at decode, scalar 0
+    dev = torch.device("cuda", 0)
+    d_r = torch.from_numpy(rounds.view(np.int64)).to(dev)
+    d_s = torch.from_numpy(sigs).to(dev)
+    d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_rand = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    stats = (ctypes.c_uint64 * 4)()
+    rc = lib.dh_verify_batch_device(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr()), ctypes.c_void_p(d_s.data_ptr()),
+                                    s.sig_len, None, 0, None, n, ctypes.c_void_p(d_v.data_ptr()),
+                                    ctypes.c_void_p(d_rand.data_ptr()), 9, None, stats)
+    assert rc == 0, _lib.last_error()
+    torch.cuda.synchronize()
+    v = d_v.cpu().numpy()
+    assert np.flatnonzero(v == 0).tolist() == [10, 2500, 4000]
+    assert stats[0] >= 2 and stats[1] >= 3 and stats[2] >= 2 and stats[3] == 3
+    host_v, _ = s.verify_beacons(pk, rounds, sigs, seed=9)
+    assert np.array_equal(host_v, v.astype(bool))
