@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Secondary BASELINE.json configs (the headline is bench.py = configs[1], quicknet 1M).
 
-    python bench/bench_configs.py unchained   [--rounds 1048576]   # configs[2] on one GPU
+    python bench/bench_configs.py unchained   [--rounds 1048576 --corrupt 0]   # configs[2] on one GPU
     python bench/bench_configs.py chained     [--rounds 1048576 --corrupt 0.001]   # configs[4] shape, one GPU
     python bench/bench_configs.py recover     [--rounds 2048 --n 64 --t 33]        # configs[3], scaled rounds
 
@@ -188,7 +188,7 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--streams", type=int, default=3)
-    ap.add_argument("--corrupt", type=float, default=0.001)
+    ap.add_argument("--corrupt", type=float, default=None, help="fraction of corrupted rounds (chained: 0.001)")
     ap.add_argument("--n", type=int, default=64)
     ap.add_argument("--t", type=int, default=33)
     ap.add_argument("--cpu-sample", type=int, default=2000)
@@ -201,7 +201,8 @@ def main():
         args.rounds = args.rounds or (1 << 20)
         name = {"unchained": "pedersen-bls-unchained", "chained": "pedersen-bls-chained",
                 "quicknet": "bls-unchained-g1-rfc9380"}[args.config]
-        out = cfg_verify(args, name, args.corrupt if args.config == "chained" else 0.0)
+        corrupt = args.corrupt if args.corrupt is not None else (0.001 if args.config == "chained" else 0.0)
+        out = cfg_verify(args, name, corrupt)
     print(json.dumps(out), flush=True)
 
 

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Bisection-ladder sweep on the chained replay (1M pedersen-bls-chained rounds, 0.1% corrupted, one stream):
-#   bash bench/bisect_sweep.sh <tag>
+# Bisection-ladder sweep over 1M corrupted rounds (chained replay by default; quicknet / unchained), one stream:
+#   bash bench/bisect_sweep.sh <tag> [chained|quicknet|unchained]
 # adaptive (default) vs the fixed r01 ladder at three fault densities set through DRANDHIP_BISECT; one JSON line per ladder.
 set -euo pipefail
 TAG=${1:-dev}
@@ -8,7 +8,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd "$R"
-ARGS="chained --streams 1 --steps 2 --warmup 1 --cpu-sample 100 --cpu-threads 4"
+CFG=${2:-chained}
+ARGS="$CFG --streams 1 --steps 2 --warmup 1 --cpu-sample 100 --cpu-threads 4"
 for C in 0.001 0.000001 0.01; do
   for L in adaptive 4096,256,16,2; do
     if [ "$L" = adaptive ]; then unset DRANDHIP_BISECT; else export DRANDHIP_BISECT=$L; fi
