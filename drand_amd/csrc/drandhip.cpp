@@ -8,7 +8,8 @@
 // Verification flow of one batch (dh_verify_batch_device):
 //   decode pk -> prep signatures (status, affine sigma, randomness) -> prep messages (Q_i, pre-cofactor)
 //   -> RLC scalars -> level 0: one group = every round: MSM + pairing check
-//   -> on failure, bisection levels with smaller groups (4096, 256, 16, 2 rounds) over the failing groups only
+//   -> on failure, bisection levels with smaller groups (sizes from an expected-cost model: 1024, then 256/64/16/4
+//      as the observed fault density says, or straight to leaves) over the failing groups only
 //   -> leaves: per-round 2-pairing checks. Verdict = decode ok AND (group passed OR leaf passed),
 //   which is the per-round VerifyBeacon verdict of /root/reference/crypto/schemes.go:70-72.
 #include <hip/hip_runtime.h>
@@ -502,7 +503,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
   HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
 
-  // bisection levels: group sizes n, 4096, 256, 16, 2, then per-round leaves (a failing group is re-checked
+  // bisection levels: group sizes n, then next_group_size() per level, then per-round leaves (a failing group is re-checked
   // as smaller groups with the same scalars; only rounds of failing pairs reach a per-round pairing check)
   size_t m = n;
   static const char* const msm_names[8] = {"msm_level0", "msm_bisect1", "msm_bisect2", "msm_bisect3",
