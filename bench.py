@@ -33,15 +33,15 @@ sys.path.insert(0, ROOT)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=12)
-    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=24)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=1 << 20, help="rounds per GPU per step")
     ap.add_argument("--scheme", default="bls-unchained-g1-rfc9380")
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--roofline-steps", type=int, default=2, help="single-stream batches timed for the roofline")
-    ap.add_argument("--streams", type=int, default=6,
+    ap.add_argument("--streams", type=int, default=8,
                     help="batches in flight per GPU (host threads, each with its own HIP stream in libdrandhip)")
     return ap.parse_args()
 
