@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stage-times", action="store_true",
+                    help="leave the library's HIP-event stage timing off inside the timed region")
     ap.add_argument("--roofline-steps", type=int, default=2, help="single-stream batches timed for the roofline")
     ap.add_argument("--streams", type=int, default=8,
                     help="batches in flight per GPU (host threads, each with its own HIP stream in libdrandhip)")
@@ -151,7 +153,7 @@ def main():
     # the timed region; W < S would leave workspace allocation inside it
     warm_batches = max(args.warmup, S) if args.warmup else 0
     run_steps(warm_batches, S)
-    lib.dh_profile(1)
+    lib.dh_profile(0 if args.no_stage_times else 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
