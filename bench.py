@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--roofline-steps", type=int, default=2, help="single-stream batches timed for the roofline")
     ap.add_argument("--streams", type=int, default=8,
                     help="batches in flight per GPU (host threads, each with its own HIP stream in libdrandhip)")
+    ap.add_argument("--split", default="0",
+                    help="DRANDHIP_SPLIT for the timed calls ('chunk,workers'; 0 = each call on one stream: the bench "
+                         "already keeps --streams calls in flight)")
     return ap.parse_args()
 
 
@@ -79,6 +82,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ["DRANDHIP_SPLIT"] = args.split  # read once, when the library first splits a call
     import torch
     import torch.distributed as dist
     from drand_amd import _lib, scheme_from_name

@@ -19,10 +19,13 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cmath>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/drandhip.h"
@@ -82,7 +85,7 @@ struct worker {
   hipStream_t stream = nullptr;
   bool busy = false;
   // per-round state
-  dbuf status, sig_aff, q_pts, scal, entries, verdict_tmp, rand_tmp;
+  dbuf status, sig_aff, q_pts, scal, entries, verdict_tmp, rand_tmp, h2c_tmp;
   // host-API staging
   dbuf in_rounds, in_sigs, in_prevs, in_prev_lens, out_verdict, out_rand;
   // key
@@ -104,7 +107,7 @@ struct worker {
   uint8_t cached_key_ok = 0;
   std::vector<uint32_t> h_entries, h_next;
   void release_all() {
-    dbuf* all[] = {&status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &in_rounds, &in_sigs,
+    dbuf* all[] = {&status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &h2c_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
@@ -120,17 +123,25 @@ struct context {
   std::mutex mu;
   bool inited = false;
   int device = 0;
-  std::vector<worker*> pool;
+  std::vector<worker*> pool;     // idle or leased workers
+  std::vector<worker*> retired;  // leased when dh_shutdown ran: freed by their lease's end
 };
 context g_ctx;
 
+// One device per process (the multi-GPU layout is one process per GPU): the mask must name at
+// most one device; 0 means "device 0, or the device already selected".
 int ensure_init_locked(uint32_t mask) {
-  if (g_ctx.inited) return DH_OK;
+  if (mask & (mask - 1)) return fail(DH_EINVAL, "device mask 0x%x names more than one device (one process per GPU)", mask);
+  const int want = mask ? __builtin_ctz(mask) : -1;
+  if (g_ctx.inited) {
+    if (want >= 0 && want != g_ctx.device)
+      return fail(DH_EINVAL, "already initialised on device %d (dh_shutdown first)", g_ctx.device);
+    return DH_OK;
+  }
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev <= 0) return fail(DH_EDEVICE, "no HIP device available (%s)", hipGetErrorString(e));
-  int dev = 0;
-  if (mask) dev = __builtin_ctz(mask);
+  const int dev = want >= 0 ? want : 0;
   if (dev >= ndev) return fail(DH_EINVAL, "device %d not present (%d devices)", dev, ndev);
   g_ctx.device = dev;
   g_ctx.inited = true;
@@ -159,6 +170,13 @@ struct lease {
     if (!w) return;
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     w->busy = false;
+    auto it = std::find(g_ctx.retired.begin(), g_ctx.retired.end(), w);
+    if (it != g_ctx.retired.end()) {  // dh_shutdown ran during this call
+      g_ctx.retired.erase(it);
+      if (w->stream) (void)hipStreamSynchronize(w->stream);
+      w->release_all();
+      delete w;
+    }
   }
 };
 
@@ -294,7 +312,7 @@ struct prof_entry {
 };
 struct profiler {
   std::mutex mu;
-  bool on = false;
+  std::atomic<bool> on{false};  // read on every launch without the lock
   std::vector<std::pair<std::string, prof_entry>> table;
   void add(const char* name, float ms) {
     std::lock_guard<std::mutex> lk(mu);
@@ -323,7 +341,7 @@ struct timed_launches {
   explicit timed_launches(hipStream_t s) : st(s) {}
   template <class F>
   hipError_t run(const char* name, F&& f) {
-    if (!g_prof.on) return f();
+    if (!g_prof.on.load(std::memory_order_relaxed)) return f();
     rec r{name, nullptr, nullptr};
     (void)hipEventCreate(&r.a);
     (void)hipEventCreate(&r.b);
@@ -442,8 +460,6 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   const int sig_len = g2 ? 96 : 48, key_len = g2 ? 48 : 96;
   if ((int)pk_len != key_len) return fail(DH_EINVAL, "public key must be %d bytes for scheme %d", key_len, scheme);
   if (sig_stride < (size_t)sig_len || sig_stride % 4) return fail(DH_EINVAL, "bad signature stride %zu", sig_stride);
-  if (scheme == DH_SCHEME_CHAINED && d_prevs && (prev_stride % 4 || (!d_prev_lens && prev_stride > 96)))
-    return fail(DH_EINVAL, "bad previous-signature stride %zu", prev_stride);
   if (stats) memset(stats, 0, 4 * sizeof(uint64_t));
   if (n == 0) return DH_OK;
   if (n >= 0x80000000u) return fail(DH_EINVAL, "batch too large");  // sorted-list entries keep a sign bit
@@ -476,16 +492,14 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>" : "k_prep_sig<fp>", [&] {
     return dh::launch_prep(g2, d_sigs, sig_stride, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), d_rand, st);
   }));
-  if (d_msgs32) {  // VerifyRecovered: the messages are given (32-byte digests), not derived from rounds
-    HIP_TRY(T.run(g2 ? "k_prep_msg32<fp2>" : "k_prep_msg32<fp>", [&] {
-      return dh::launch_msg32(g2, d_msgs32, n, dst_id(scheme), w->q_pts.as<uint32_t>(), st);
-    }));
-  } else {
-    HIP_TRY(T.run(g2 ? "k_prep_msg<fp2>" : "k_prep_msg<fp>", [&] {
-      return dh::launch_msg(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, n,
-                            scheme == DH_SCHEME_CHAINED && d_prevs ? 1 : 0, dst_id(scheme), w->q_pts.as<uint32_t>(), st);
-    }));
-  }
+  // hash points: of the beacon digests, or of the given 32-byte messages (VerifyRecovered); a chained record
+  // longer than its slot rejects its round (status)
+  HIP_TRY(w->h2c_tmp.ensure(dh::hash_tmp_bytes(g2, n)));
+  HIP_TRY(T.run(d_msgs32 ? (g2 ? "k_prep_msg32<fp2>" : "k_prep_msg32<fp>") : (g2 ? "k_prep_msg<fp2>" : "k_prep_msg<fp>"), [&] {
+    return dh::launch_hash(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, d_msgs32, n,
+                           scheme == DH_SCHEME_CHAINED && d_prevs && !d_msgs32 ? 1 : 0, dst_id(scheme), w->status.as<uint8_t>(),
+                           w->q_pts.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), st);
+  }));
   uint32_t seedw[8];
   int rc = make_seed(seed, seedw);
   if (rc) return rc;
@@ -798,8 +812,10 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   HIP_TRY(w->r_msgs.ensure(n_rounds * 32));
   HIP_TRY(w->r_q.ensure(n_rounds * jw * 4));
   HIP_TRY(hipMemcpyAsync(w->r_msgs.p, msgs32, n_rounds * 32, hipMemcpyHostToDevice, st));
+  HIP_TRY(w->h2c_tmp.ensure(dh::hash_tmp_bytes(g2, n_rounds)));
   HIP_TRY(T.run(g2 ? "k_prep_msg32<fp2>" : "k_prep_msg32<fp>", [&] {
-    return dh::launch_msg32(g2, w->r_msgs.as<uint8_t>(), n_rounds, dst_id(scheme), w->r_q.as<uint32_t>(), st);
+    return dh::launch_hash(g2, nullptr, nullptr, 0, nullptr, w->r_msgs.as<uint8_t>(), n_rounds, 0, dst_id(scheme), nullptr,
+                           w->r_q.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), st);
   }));
   // 6. per-partial round, share index (host parse), signer-sorted entry lists
   std::vector<uint32_t> round_of(np), share(np);
@@ -986,6 +1002,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(w->r_entries2.ensure(n_rounds * 4));
     HIP_TRY(dh::launch_prep(g2, w->r_sigbytes.as<uint8_t>(), sl, n_rounds, w->r_status2.as<uint8_t>(),
                             w->r_aff2.as<uint32_t>(), nullptr, st));
+    HIP_TRY(w->r_scal.ensure(std::max(np, n_rounds) * 16 + 16));  // rounds may outnumber the partials
     HIP_TRY(dh::launch_scalars(d_seed, n_rounds, w->r_status2.as<uint8_t>(), w->r_scal.as<uint4>(), st));
     HIP_TRY(dh::launch_iota(w->r_entries2.as<uint32_t>(), n_rounds, st));
     // group key = commit 0 (affine, key group) — staged where the group check expects it
@@ -1033,6 +1050,80 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   return DH_OK;
 }
 
+// ---- one call over many internal streams (the drop-in callers make ONE call per window)
+// A batch of n rounds is cut into chunks verified concurrently by up to `workers` leased workers (each its own
+// HIP stream and workspace), so a single dh_verify_batch gets the overlap the bench gets from several calls in
+// flight: one chunk's latency-bound group check runs beside the next chunk's per-round kernels. Every chunk is
+// a complete batch check (its own RLC scalars: seed + chunk index when the caller fixed a seed, fresh CSPRNG
+// seeds otherwise), so verdicts stay bit-exact per round. DRANDHIP_SPLIT="chunk,workers" overrides the
+// defaults (262144 rounds, 8 workers); "0" disables splitting.
+struct split_cfg {
+  size_t chunk = 262144;
+  int workers = 8;
+};
+static const split_cfg& split_config() {
+  static const split_cfg c = [] {
+    split_cfg r;
+    const char* e = getenv("DRANDHIP_SPLIT");
+    if (e && *e) {
+      char* end = nullptr;
+      r.chunk = strtoull(e, &end, 10);
+      if (end && *end == ',') r.workers = std::max(1, atoi(end + 1));
+    }
+    return r;
+  }();
+  return c;
+}
+
+int ensure_device() {
+  std::lock_guard<std::mutex> lk(g_ctx.mu);
+  int rc = ensure_init_locked(0);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(g_ctx.device));
+  return DH_OK;
+}
+
+template <class F>
+int run_split(size_t n, F&& fn, uint64_t seed) {
+  const split_cfg& cfg = split_config();
+  size_t nchunks = 1;
+  if (cfg.chunk && cfg.workers > 1 && n >= 2 * cfg.chunk) nchunks = (n + cfg.chunk - 1) / cfg.chunk;
+  const size_t per = (n + nchunks - 1) / std::max<size_t>(nchunks, 1);
+  const int nthreads = (int)std::min<size_t>(nchunks, (size_t)cfg.workers);
+  std::atomic<size_t> next{0};
+  std::atomic<int> first_rc{DH_OK};
+  std::mutex err_mu;
+  std::string err;
+  auto body = [&]() {
+    lease L;
+    int rc = L.rc ? L.rc : set_device_and_stream(L.w);
+    for (size_t c; !rc && (c = next.fetch_add(1)) < nchunks;) {
+      const size_t lo = c * per, hi = std::min(n, lo + per);
+      if (lo >= hi) continue;
+      rc = fn(L.w, lo, hi, seed ? seed + 0x9e3779b97f4a7c15ULL * c : 0);
+    }
+    if (rc) {
+      int expect = DH_OK;
+      if (first_rc.compare_exchange_strong(expect, rc)) {
+        std::lock_guard<std::mutex> lk(err_mu);
+        err = g_err;  // the message lives in this thread's g_err: hand it to the caller's
+      }
+      next.store(nchunks);  // stop the other workers early
+    }
+  };
+  if (nthreads <= 1) {
+    body();
+  } else {
+    std::vector<std::thread> ths;
+    for (int t = 1; t < nthreads; t++) ths.emplace_back(body);
+    body();
+    for (auto& th : ths) th.join();
+  }
+  const int rc = first_rc.load();
+  if (rc) g_err = err;
+  return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1043,8 +1134,14 @@ int dh_init(uint32_t device_mask) {
 }
 
 void dh_shutdown(void) {
+  // idle workers are freed now; a worker leased by a call still running on another thread is retired and freed
+  // when that call returns, so the call never touches freed memory
   std::lock_guard<std::mutex> lk(g_ctx.mu);
   for (worker* w : g_ctx.pool) {
+    if (w->busy) {
+      g_ctx.retired.push_back(w);
+      continue;
+    }
     w->release_all();
     delete w;
   }
@@ -1076,13 +1173,33 @@ int dh_verify_batch_device(int scheme, const uint8_t* pk, size_t pk_len, const u
                            uint64_t stats_out[4]) {
   if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
   if (!pk || (n && (!d_rounds || !d_sigs || !d_verdict_out))) return fail(DH_EINVAL, "null argument");
-  lease L;
-  if (L.rc) return L.rc;
-  int rc = set_device_and_stream(L.w);
-  if (rc) return rc;
-  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : L.w->stream;
-  return verify_core(L.w, scheme, pk, pk_len, d_rounds, d_sigs, sig_stride, d_prevs, prev_stride, d_prev_lens, n,
-                     d_verdict_out, d_rand_out, seed, st, stats_out);
+  if (stats_out) memset(stats_out, 0, 4 * sizeof(uint64_t));
+  // inputs produced on the caller's stream: every internal stream waits for that stream's work first
+  hipEvent_t ready = nullptr;
+  if (hip_stream) {
+    int rc0 = ensure_device();
+    if (rc0) return rc0;
+    HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ready, (hipStream_t)hip_stream));
+  }
+  std::mutex stats_mu;
+  int rc = run_split(n, [&](worker* w, size_t lo, size_t hi, uint64_t chunk_seed) -> int {
+    if (ready) HIP_TRY(hipStreamWaitEvent(w->stream, ready, 0));
+    uint64_t st4[4];
+    const bool chained = scheme == DH_SCHEME_CHAINED && d_prevs;
+    int r = verify_core(w, scheme, pk, pk_len, d_rounds + lo, d_sigs + lo * sig_stride, sig_stride,
+                        chained ? d_prevs + lo * prev_stride : nullptr,
+                        prev_stride, chained && d_prev_lens ? d_prev_lens + lo : nullptr, hi - lo, d_verdict_out + lo,
+                        d_rand_out ? d_rand_out + lo * 32 : nullptr, chunk_seed, w->stream, stats_out ? st4 : nullptr);
+    if (!r && stats_out) {
+      std::lock_guard<std::mutex> lk(stats_mu);
+      stats_out[0] = std::max(stats_out[0], st4[0]);
+      for (int k = 1; k < 4; k++) stats_out[k] += st4[k];
+    }
+    return r;
+  }, seed);
+  if (ready) (void)hipEventDestroy(ready);
+  return rc;
 }
 
 int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* rounds, const uint8_t* sigs,
@@ -1091,39 +1208,39 @@ int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t
   if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
   if (!pk || (n && (!rounds || !sigs || !verdict_out))) return fail(DH_EINVAL, "null argument");
   if (n == 0) return DH_OK;
-  lease L;
-  if (L.rc) return L.rc;
-  worker* w = L.w;
-  int rc = set_device_and_stream(w);
-  if (rc) return rc;
-  hipStream_t st = w->stream;
   const bool chained = scheme == DH_SCHEME_CHAINED && prevs;
-  HIP_TRY(w->in_rounds.ensure(n * 8));
-  HIP_TRY(w->in_sigs.ensure(n * sig_stride));
-  HIP_TRY(w->out_verdict.ensure(n));
-  if (rand_out) HIP_TRY(w->out_rand.ensure(n * 32));
-  HIP_TRY(hipMemcpyAsync(w->in_rounds.p, rounds, n * 8, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(w->in_sigs.p, sigs, n * sig_stride, hipMemcpyHostToDevice, st));
-  if (chained) {
-    HIP_TRY(w->in_prevs.ensure(n * prev_stride + 4));
-    HIP_TRY(hipMemcpyAsync(w->in_prevs.p, prevs, n * prev_stride, hipMemcpyHostToDevice, st));
-    if (prev_lens) {
-      for (size_t i = 0; i < n; i++)
-        if (prev_lens[i] % 4 || prev_lens[i] > 96 || prev_lens[i] > prev_stride)
-          return fail(DH_EINVAL, "previous signature %zu has unsupported length %u", i, prev_lens[i]);
-      HIP_TRY(w->in_prev_lens.ensure(n * 4));
-      HIP_TRY(hipMemcpyAsync(w->in_prev_lens.p, prev_lens, n * 4, hipMemcpyHostToDevice, st));
+  if (chained && prev_lens)
+    for (size_t i = 0; i < n; i++)
+      if (prev_lens[i] > prev_stride)
+        return fail(DH_EINVAL, "previous signature %zu: length %u exceeds the record stride %zu", i, prev_lens[i], prev_stride);
+  // one chunk per worker at a time: its host->device copies overlap the other chunks' kernels
+  return run_split(n, [&](worker* w, size_t lo, size_t hi, uint64_t chunk_seed) -> int {
+    const size_t m = hi - lo;
+    hipStream_t st = w->stream;
+    HIP_TRY(w->in_rounds.ensure(m * 8));
+    HIP_TRY(w->in_sigs.ensure(m * sig_stride));
+    HIP_TRY(w->out_verdict.ensure(m));
+    if (rand_out) HIP_TRY(w->out_rand.ensure(m * 32));
+    HIP_TRY(hipMemcpyAsync(w->in_rounds.p, rounds + lo, m * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(w->in_sigs.p, sigs + lo * sig_stride, m * sig_stride, hipMemcpyHostToDevice, st));
+    if (chained) {
+      HIP_TRY(w->in_prevs.ensure(m * prev_stride + 4));
+      HIP_TRY(hipMemcpyAsync(w->in_prevs.p, prevs + lo * prev_stride, m * prev_stride, hipMemcpyHostToDevice, st));
+      if (prev_lens) {
+        HIP_TRY(w->in_prev_lens.ensure(m * 4));
+        HIP_TRY(hipMemcpyAsync(w->in_prev_lens.p, prev_lens + lo, m * 4, hipMemcpyHostToDevice, st));
+      }
     }
-  }
-  rc = verify_core(w, scheme, pk, pk_len, w->in_rounds.as<uint64_t>(), w->in_sigs.as<uint8_t>(), sig_stride,
-                   chained ? w->in_prevs.as<uint8_t>() : nullptr, prev_stride,
-                   chained && prev_lens ? w->in_prev_lens.as<uint32_t>() : nullptr, n, w->out_verdict.as<uint8_t>(),
-                   rand_out ? w->out_rand.as<uint8_t>() : nullptr, seed, st, nullptr);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(verdict_out, w->out_verdict.p, n, hipMemcpyDeviceToHost, st));
-  if (rand_out) HIP_TRY(hipMemcpyAsync(rand_out, w->out_rand.p, n * 32, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  return DH_OK;
+    int rc = verify_core(w, scheme, pk, pk_len, w->in_rounds.as<uint64_t>(), w->in_sigs.as<uint8_t>(), sig_stride,
+                         chained ? w->in_prevs.as<uint8_t>() : nullptr, prev_stride,
+                         chained && prev_lens ? w->in_prev_lens.as<uint32_t>() : nullptr, m, w->out_verdict.as<uint8_t>(),
+                         rand_out ? w->out_rand.as<uint8_t>() : nullptr, chunk_seed, st, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(verdict_out + lo, w->out_verdict.p, m, hipMemcpyDeviceToHost, st));
+    if (rand_out) HIP_TRY(hipMemcpyAsync(rand_out + lo * 32, w->out_rand.p, m * 32, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return DH_OK;
+  }, seed);
 }
 
 int dh_verify_beacon(int scheme, const uint8_t* pk, size_t pk_len, uint64_t round, const uint8_t* sig, size_t sig_len,
@@ -1132,17 +1249,18 @@ int dh_verify_beacon(int scheme, const uint8_t* pk, size_t pk_len, uint64_t roun
   if (sl < 0) return sl;
   if (!sig || sig_len != (size_t)sl) return 0;  // kyber: wrong-length signature is an invalid signature
   uint8_t sbuf[96] __attribute__((aligned(16)));
-  uint8_t pbuf[96] __attribute__((aligned(16)));
   memcpy(sbuf, sig, sig_len);
+  // the previous signature is hashed whatever its length (crypto/schemes.go:106-114)
+  if (scheme == DH_SCHEME_CHAINED && prev_len > 0xffffffffu) return fail(DH_EINVAL, "previous signature too long");
+  std::vector<uint8_t> pbuf(std::max<size_t>(96, (prev_len + 3) & ~(size_t)3), 0);
   uint32_t plen = 0;
   if (scheme == DH_SCHEME_CHAINED && prev && prev_len) {
-    if (prev_len % 4 || prev_len > 96) return fail(DH_EINVAL, "unsupported previous-signature length %zu", prev_len);
-    memcpy(pbuf, prev, prev_len);
+    memcpy(pbuf.data(), prev, prev_len);
     plen = (uint32_t)prev_len;
   }
   uint8_t verdict = 0;
-  int rc = dh_verify_batch(scheme, pk, pk_len, &round, sbuf, (size_t)sl, scheme == DH_SCHEME_CHAINED ? pbuf : nullptr, 96,
-                           scheme == DH_SCHEME_CHAINED ? &plen : nullptr, 1, &verdict, nullptr, 0);
+  int rc = dh_verify_batch(scheme, pk, pk_len, &round, sbuf, (size_t)sl, scheme == DH_SCHEME_CHAINED ? pbuf.data() : nullptr,
+                           pbuf.size(), scheme == DH_SCHEME_CHAINED ? &plen : nullptr, 1, &verdict, nullptr, 0);
   return rc < 0 ? rc : verdict;
 }
 
@@ -1191,6 +1309,7 @@ int dh_digest_batch(int scheme, const uint64_t* rounds, const uint8_t* prevs, si
     s.init();
     if (scheme == DH_SCHEME_CHAINED && prevs) {
       size_t pl = prev_lens ? prev_lens[i] : prev_stride;
+      if (pl > prev_stride) return fail(DH_EINVAL, "previous signature %zu: length %zu exceeds the record stride %zu", i, pl, prev_stride);
       s.update(prevs + i * prev_stride, pl);
     }
     uint8_t r[8];
@@ -1272,8 +1391,6 @@ int dh_sign_batch(int scheme, const uint8_t* sk32, const uint64_t* rounds, const
   if (!sk32 || (n && (!rounds || !sigs_out))) return fail(DH_EINVAL, "null argument");
   if (n == 0) return DH_OK;
   const bool chained = scheme == DH_SCHEME_CHAINED && prevs;
-  if (chained && (prev_stride % 4 || (!prev_lens && prev_stride > 96)))
-    return fail(DH_EINVAL, "bad previous-signature stride %zu", prev_stride);
   lease L;
   if (L.rc) return L.rc;
   worker* w = L.w;
@@ -1292,16 +1409,20 @@ int dh_sign_batch(int scheme, const uint8_t* sk32, const uint64_t* rounds, const
     HIP_TRY(hipMemcpyAsync(w->in_prevs.p, prevs, n * prev_stride, hipMemcpyHostToDevice, st));
     if (prev_lens) {
       for (size_t i = 0; i < n; i++)
-        if (prev_lens[i] % 4 || prev_lens[i] > 96 || prev_lens[i] > prev_stride)
-          return fail(DH_EINVAL, "previous signature %zu has unsupported length %u", i, prev_lens[i]);
+        if (prev_lens[i] > prev_stride)
+          return fail(DH_EINVAL, "previous signature %zu: length %u exceeds the record stride %zu", i, prev_lens[i], prev_stride);
       HIP_TRY(w->in_prev_lens.ensure(n * 4));
       HIP_TRY(hipMemcpyAsync(w->in_prev_lens.p, prev_lens, n * 4, hipMemcpyHostToDevice, st));
     }
   }
+  if (sl == 96) {
+    HIP_TRY(w->q_pts.ensure(n * JAC_WORDS_G2 * 4));
+    HIP_TRY(w->h2c_tmp.ensure(dh::hash_tmp_bytes(1, n)));
+  }
   HIP_TRY(dh::launch_sign(sl == 96, w->key_ok.as<uint32_t>(), w->in_rounds.as<uint64_t>(),
                           chained ? w->in_prevs.as<uint8_t>() : nullptr, prev_stride,
-                          chained && prev_lens ? w->in_prev_lens.as<uint32_t>() : nullptr, n, chained ? 1 : 0,
-                          dst_id(scheme), w->in_sigs.as<uint8_t>(), st));
+                          chained && prev_lens ? w->in_prev_lens.as<uint32_t>() : nullptr, nullptr, n, chained ? 1 : 0,
+                          dst_id(scheme), w->in_sigs.as<uint8_t>(), w->q_pts.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), st));
   HIP_TRY(hipMemcpyAsync(sigs_out, w->in_sigs.p, n * sl, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   return DH_OK;

@@ -166,12 +166,24 @@ DH_DEV fp fp_mul_cios(const fp& a, const fp& b) {
   return r;
 }
 
-// The field product used everywhere: product-scanning Montgomery (fp_mul_fips.hpp), called through
-// an out-of-line function with a register-passing vector ABI so that the large kernels (pairing,
-// hash-to-curve) stay compact; define DH_MUL_INLINE to inline it instead.
+// The field product used everywhere: product-scanning Montgomery (fp_mul_fips.hpp), one out-of-line copy
+// per code object so that the large kernels (pairing, hash-to-curve) stay compact; define DH_MUL_INLINE to
+// inline it instead.
+//
+// Call convention. A plain call makes the caller assume the standard AMDGPU C convention: every
+// caller-saved VGPR (v0-v39 and the v48-55, v64-71, ... stripes, ~148 registers) dies at the call, so
+// only ~108 VGPRs can carry values across a product — 4 Fp2 elements. The G2 point formulas keep more
+// than that live and spilled to scratch around EVERY product (k_prep_msg<fp2>: 19.3 KB of scratch per
+// lane). The products are therefore entered through an inline-asm `s_swappc_b64` whose clobber list is
+// exactly what the two bodies touch: v0-v39, v48, s0-s15, s30-s31, vcc and scc (the squaring also v49-55,
+// v64-71, v80-81). The bodies are ordinary compiled functions: they may set SCC and mask EXEC around a
+// branch (restoring it), so SCC must be in the list — without it a loop condition held in SCC across a
+// product was lost. Everything else stays live in registers across the call. drand_amd/tools/check_fp_abi.py
+// disassembles every built code object and fails the build if a body touches a register outside that list,
+// leaves EXEC modified, uses the stack or calls out, so a compiler change cannot silently break the contract.
 typedef uint32_t fpvec __attribute__((ext_vector_type(12)));
 
-__device__ __noinline__ fpvec fp_mul_vec(fpvec a, fpvec b) {
+extern "C" __device__ __noinline__ __attribute__((used)) fpvec dh_fp_mul_vec(fpvec a, fpvec b) {
   uint32_t x[12], y[12], r[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) { x[i] = a[i]; y[i] = b[i]; }
@@ -181,7 +193,7 @@ __device__ __noinline__ fpvec fp_mul_vec(fpvec a, fpvec b) {
   for (int i = 0; i < 12; i++) o[i] = r[i];
   return o;
 }
-__device__ __noinline__ fpvec fp_sqr_vec(fpvec a) {
+extern "C" __device__ __noinline__ __attribute__((used)) fpvec dh_fp_sqr_vec(fpvec a) {
   uint32_t x[12], r[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) x[i] = a[i];
@@ -191,6 +203,20 @@ __device__ __noinline__ fpvec fp_sqr_vec(fpvec a) {
   for (int i = 0; i < 12; i++) o[i] = r[i];
   return o;
 }
+
+#define DH_FP_CALL_CLOBBERS                                                                                    \
+  "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", \
+      "v48", "s0", "s1", "s2", "s3", "s4", "s5", "s6", "s7", "s8", "s9", "s10", "s11", "s12", "s13", "s14", "s15",  \
+      "s30", "s31", "vcc", "scc"
+// the squaring's body also works in the caller-saved stripes v49-v55, v64-v71, v80-v81
+#define DH_FP_SQR_EXTRA_CLOBBERS                                                                                  \
+  "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v80", \
+      "v81"
+// a = a * b (a in v0-v11, b in v12-v23 and clobbered); the callee address is formed exactly as the compiler
+// forms it for a direct call
+#define DH_FP_CALL(fn) \
+  "s_getpc_b64 s[14:15]\n\ts_add_u32 s14, s14, " fn "@rel32@lo+4\n\ts_addc_u32 s15, s15, " fn "@rel32@hi+12\n\ts_swappc_b64 s[30:31], s[14:15]"
+
 DH_DEV fpvec to_vec(const fp& a) {
   fpvec v;
 #pragma unroll
@@ -210,7 +236,9 @@ DH_DEV fp fp_mul(const fp& a, const fp& b) {
   fips_mont_mul(r.v, a.v, b.v);
   return r;
 #else
-  return from_vec(fp_mul_vec(to_vec(a), to_vec(b)));
+  fpvec x = to_vec(a), y = to_vec(b);
+  asm(DH_FP_CALL("dh_fp_mul_vec") : "+{v[0:11]}"(x), "+{v[12:23]}"(y) : : DH_FP_CALL_CLOBBERS);
+  return from_vec(x);
 #endif
 }
 
@@ -220,7 +248,13 @@ DH_DEV fp fp_sqr(const fp& a) {
   fips_mont_sqr(r.v, a.v);
   return r;
 #else
-  return from_vec(fp_sqr_vec(to_vec(a)));
+  fpvec x = to_vec(a);
+  asm(DH_FP_CALL("dh_fp_sqr_vec")
+      : "+{v[0:11]}"(x)
+      :
+      : "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", DH_FP_CALL_CLOBBERS,
+        DH_FP_SQR_EXTRA_CLOBBERS);
+  return from_vec(x);
 #endif
 }
 

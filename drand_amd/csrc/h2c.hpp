@@ -205,6 +205,46 @@ DH_DEV jac<fp2> iso3_jac(const jac<fp2>& p) {
   return r;
 }
 
+// Register-lean forms for the G2 pass kernels (k_prep.hip): the same maps as iso3_jac / jac_add_distinct with
+// the operations reordered so that at most ~7 Fp2 values are live at once (one lane holds ~10 in 256 VGPRs).
+// Same points; the Jacobian representatives differ (Z scaled), which no consumer depends on.
+//
+// iso3 with the y-part first: Ny = Y yn and yd Z^3 collapse before the x-part's Horner runs.
+DH_DEV jac<fp2> iso3_jac_lean(const jac<fp2>& p) {
+  using namespace cst;
+  const fp2 D = fp2_sqr(p.z);
+  fp2 ydz3;
+  fp2 ny;
+  {
+    fp2 yn = fp2_c(ISO3_YNUM[ISO3_YNUM_LEN - 1]);
+    fp2 yd = fp2_c(ISO3_YDEN[ISO3_YDEN_LEN - 1]);
+    fp2 zp = D;
+#pragma unroll 1
+    for (int j = 1; j < ISO3_YNUM_LEN; j++) {
+      if (j > 1) zp = fp2_mul(zp, D);
+      yn = fp2_add(fp2_mul(yn, p.x), fp2_mul(fp2_c(ISO3_YNUM[ISO3_YNUM_LEN - 1 - j]), zp));
+      yd = fp2_add(fp2_mul(yd, p.x), fp2_mul(fp2_c(ISO3_YDEN[ISO3_YDEN_LEN - 1 - j]), zp));
+    }
+    ydz3 = fp2_mul(yd, fp2_mul(D, p.z));
+    ny = fp2_mul(p.y, yn);
+  }
+  fp2 xn = fp2_c(ISO3_XNUM[ISO3_XNUM_LEN - 1]);
+  fp2 xd = fp2_c(ISO3_XDEN[ISO3_XDEN_LEN - 1]);
+  fp2 zp = D;
+#pragma unroll 1
+  for (int j = 1; j < ISO3_XNUM_LEN; j++) {
+    if (j > 1) zp = fp2_mul(zp, D);
+    xn = fp2_add(fp2_mul(xn, p.x), fp2_mul(fp2_c(ISO3_XNUM[ISO3_XNUM_LEN - 1 - j]), zp));
+    if (j < ISO3_XDEN_LEN) xd = fp2_add(fp2_mul(xd, p.x), fp2_mul(fp2_c(ISO3_XDEN[ISO3_XDEN_LEN - 1 - j]), zp));
+  }
+  const fp2 a = fp2_mul(xd, D);
+  jac<fp2> r;
+  r.z = fp2_mul(a, ydz3);
+  r.x = fp2_mul(fp2_mul(xn, ydz3), r.z);
+  r.y = fp2_mul(fp2_mul(ny, a), fp2_sqr(r.z));
+  return r;
+}
+
 // hash_to_curve(G2) without clear_cofactor, one isogeny after the addition on E2' (see h2c_g1_noclear)
 DH_DEV jac<fp2> h2c_g2_noclear(const sha_h& digest, int dst_id) {
   uint32_t b[8][8];

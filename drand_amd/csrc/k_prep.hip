@@ -43,39 +43,69 @@ __global__ __launch_bounds__(256, occ<F>::W) void k_prep_sig(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------- prep: messages -> hash points (no cofactor)
-template <class F>
-__global__ __launch_bounds__(256, occ<F>::W) void k_prep_msg(const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs,
-                                                  size_t prev_stride, const uint32_t* __restrict__ prev_lens, size_t n,
-                                                  int chained, int dst_id, uint32_t* __restrict__ q_out) {
+// G1 (fused): hash_to_curve without clear_cofactor, one round per lane
+__global__ __launch_bounds__(256, occ<fp>::W) void k_prep_msg_g1(const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs,
+                                                            size_t prev_stride, const uint32_t* __restrict__ prev_lens,
+                                                            const uint8_t* __restrict__ msgs32, size_t n, int chained, int dst_id,
+                                                            uint8_t* __restrict__ status, uint32_t* __restrict__ q_out) {
   size_t i = gtid();
   if (i >= n) return;
-  sha_h d;
-  if (chained) {
-    uint32_t pl = prev_lens ? prev_lens[i] : (uint32_t)prev_stride;
-    d = digest_chained(prevs + i * prev_stride, pl, rounds[i]);
-  } else {
-    d = digest_unchained(rounds[i]);
-  }
-  if constexpr (sizeof(F) == sizeof(fp)) {
-    st_jac_aos<fp>(q_out, i, h2c_g1_noclear(d, dst_id));
-  } else {
-    st_jac_aos<fp2>(q_out, i, h2c_g2_noclear(d, dst_id));
-  }
+  const sha_h d = message_of(rounds, prevs, prev_stride, prev_lens, msgs32, chained, i, status);
+  st_jac_aos<fp>(q_out, i, h2c_g1_noclear(d, dst_id));
 }
 
-// hash points for caller-given 32-byte messages (tbls: the DigestBeacon of each round)
-template <class F>
-__global__ __launch_bounds__(256, occ<F>::W) void k_prep_msg32(const uint8_t* __restrict__ msgs, size_t n, int dst_id,
-                                                       uint32_t* __restrict__ q_out) {
+// G2 in three passes. The G2 map keeps more Fp2 values live than one lane's 256 VGPRs hold (fused, the kernel
+// needed 19.3 KB of scratch per lane, and 8 such 1M-round dispatches in flight failed to launch), so the state
+// between the passes goes through HBM: u0, u1 (192 B per round) and the two SSWU points on E2' (576 B per
+// round), each written and read once (~1.5 KB per round against ~1.3 M integer products of work).
+// pass 1: message -> expand_message_xmd -> hash_to_field: u0, u1 (Montgomery Fp2), 48 words per round
+__global__ __launch_bounds__(256) void k_h2f_g2(const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs,
+                                                size_t prev_stride, const uint32_t* __restrict__ prev_lens,
+                                                const uint8_t* __restrict__ msgs32, size_t n, int chained, int dst_id,
+                                                uint8_t* __restrict__ status, uint32_t* __restrict__ u_out) {
   size_t i = gtid();
   if (i >= n) return;
-  sha_h d;
-#pragma unroll
-  for (int j = 0; j < 8; j++) d.h[j] = ld_be32a(msgs + 32 * i + 4 * j);
-  if constexpr (sizeof(F) == sizeof(fp)) {
-    st_jac_aos<fp>(q_out, i, h2c_g1_noclear(d, dst_id));
-  } else {
-    st_jac_aos<fp2>(q_out, i, h2c_g2_noclear(d, dst_id));
+  const sha_h d = message_of(rounds, prevs, prev_stride, prev_lens, msgs32, chained, i, status);
+  uint32_t b[8][8];
+  xmd32<8>(b, d, dst_id);
+  const fp2 u0 = {fp_from_be512(b[0], b[1]), fp_from_be512(b[2], b[3])};
+  const fp2 u1 = {fp_from_be512(b[4], b[5]), fp_from_be512(b[6], b[7])};
+  st_f<fp2>(u_out + 48 * i, u0);
+  st_f<fp2>(u_out + 48 * i + 24, u1);
+}
+
+// pass 2: one SSWU map per lane (2 per round), the point on E2' as Jacobian (Z = xd)
+__global__ __launch_bounds__(256, 2) void k_sswu_g2(const uint32_t* __restrict__ u, size_t m, uint32_t* __restrict__ pts) {
+  size_t j = gtid();
+  if (j >= m) return;
+  fp2 x;
+  ld_f<fp2>(x, u + 24 * j);
+  st_jac_aos<fp2>(pts, j, swu_jac(sswu_g2(x)));
+}
+
+// pass 3: Q = iso3(P0 + P1) (h2c_g2_noclear's order: one isogeny after the addition on E2'). When the two SSWU
+// points share x (never for honest inputs) the round is listed in exc[] and k_add_iso_g2_exc takes the textbook
+// order, two isogenies then the addition on E2, on a small grid.
+__global__ __launch_bounds__(256, 2) void k_add_iso_g2(const uint32_t* __restrict__ pts, size_t n, uint32_t* __restrict__ q_out,
+                                                       uint32_t* __restrict__ exc) {
+  size_t i = gtid();
+  if (i >= n) return;
+  jac<fp2> s;
+  if (!jac_add_distinct_mem(s, pts + 144 * i, pts + 144 * i + 72)) {
+    exc[1 + atomicAdd(exc, 1u)] = (uint32_t)i;
+    return;
+  }
+  st_jac_aos<fp2>(q_out, i, iso3_jac_lean(s));
+}
+
+constexpr unsigned EXC_THREADS = 64;
+__global__ __launch_bounds__(EXC_THREADS, 1) void k_add_iso_g2_exc(const uint32_t* __restrict__ pts, const uint32_t* __restrict__ exc,
+                                                                   uint32_t* __restrict__ q_out) {
+  const uint32_t cnt = exc[0];
+  for (uint32_t k = threadIdx.x; k < cnt; k += EXC_THREADS) {
+    const uint32_t i = exc[1 + k];
+    const jac<fp2> p0 = ld_jac_aos<fp2>(pts, 2 * (size_t)i), p1 = ld_jac_aos<fp2>(pts, 2 * (size_t)i + 1);
+    st_jac_aos<fp2>(q_out, i, jac_add(iso3_jac(p0), iso3_jac(p1)));
   }
 }
 
@@ -132,19 +162,6 @@ hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n,
 }
 
 
-hipError_t launch_msg(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
-                      size_t n, int chained, int dst_id, uint32_t* q_out, hipStream_t st) {
-  if (!n) return hipSuccess;
-  if (sig_g2)
-    hipLaunchKernelGGL(k_prep_msg<fp2>, dim3(nblk(n, 256)), dim3(256), 0, st, rounds, prevs, prev_stride, prev_lens, n,
-                       chained, dst_id, q_out);
-  else
-    hipLaunchKernelGGL(k_prep_msg<fp>, dim3(nblk(n, 256)), dim3(256), 0, st, rounds, prevs, prev_stride, prev_lens, n,
-                       chained, dst_id, q_out);
-  return hipGetLastError();
-}
-
-
 hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, hipStream_t st) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_scalars, dim3(nblk(n, 256)), dim3(256), 0, st, seed_words, n, status, scal);
@@ -159,10 +176,27 @@ hipError_t launch_decode_key(int key_g2, const uint8_t* pk, uint32_t* key_aff, u
 }
 
 
-hipError_t launch_msg32(int sig_g2, const uint8_t* msgs, size_t n, int dst_id, uint32_t* q_out, hipStream_t st) {
+// G2: the SSWU points (2 x 72 words per round), then the exceptional-round list (count + n indices)
+size_t hash_tmp_bytes(int sig_g2, size_t n) { return sig_g2 ? n * 2 * 72 * 4 + (n + 1) * 4 : 0; }
+
+hipError_t launch_hash(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
+                       const uint8_t* msgs32, size_t n, int chained, int dst_id, uint8_t* status, uint32_t* q_out, uint32_t* tmp,
+                       hipStream_t st) {
   if (!n) return hipSuccess;
-  if (sig_g2) hipLaunchKernelGGL(k_prep_msg32<fp2>, dim3(nblk(n, 256)), dim3(256), 0, st, msgs, n, dst_id, q_out);
-  else hipLaunchKernelGGL(k_prep_msg32<fp>, dim3(nblk(n, 256)), dim3(256), 0, st, msgs, n, dst_id, q_out);
+  if (!sig_g2) {
+    hipLaunchKernelGGL(k_prep_msg_g1, dim3(nblk(n, 256)), dim3(256), 0, st, rounds, prevs, prev_stride, prev_lens, msgs32, n,
+                       chained, dst_id, status, q_out);
+    return hipGetLastError();
+  }
+  // u0, u1 of round i go to q_out (48 of its 72 words per round), the SSWU points to tmp
+  hipLaunchKernelGGL(k_h2f_g2, dim3(nblk(n, 256)), dim3(256), 0, st, rounds, prevs, prev_stride, prev_lens, msgs32, n, chained,
+                     dst_id, status, q_out);
+  hipLaunchKernelGGL(k_sswu_g2, dim3(nblk(2 * n, 256)), dim3(256), 0, st, (const uint32_t*)q_out, 2 * n, tmp);
+  uint32_t* exc = tmp + n * 2 * 72;
+  hipError_t e = hipMemsetAsync(exc, 0, 4, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_add_iso_g2, dim3(nblk(n, 256)), dim3(256), 0, st, (const uint32_t*)tmp, n, q_out, exc);
+  hipLaunchKernelGGL(k_add_iso_g2_exc, dim3(1), dim3(EXC_THREADS), 0, st, (const uint32_t*)tmp, (const uint32_t*)exc, q_out);
   return hipGetLastError();
 }
 

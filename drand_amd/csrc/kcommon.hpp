@@ -78,6 +78,42 @@ DH_DEV void st_aff_aos(uint32_t* base, size_t i, const aff<F>& a) {
   st_f<F>(p + N, a.y);
 }
 
+// add-2007-bl for two points held in memory (AoS Jacobian, 72 words each), coordinates loaded as they are needed;
+// Z3 = 2 Z1 Z2 h (= ((Z1 + Z2)^2 - Z1^2 - Z2^2) h). false (r unset) when x1 == x2, as jac_add_distinct.
+DH_DEV bool jac_add_distinct_mem(jac<fp2>& r, const uint32_t* P, const uint32_t* Q) {
+  fp2 c1, c2, zz, u1, h;
+  {
+    fp2 z1, z2;
+    ld_f<fp2>(z1, P + 48);
+    ld_f<fp2>(z2, Q + 48);
+    const fp2 z1z1 = fp2_sqr(z1), z2z2 = fp2_sqr(z2);
+    c1 = fp2_mul(z1, z1z1);
+    c2 = fp2_mul(z2, z2z2);
+    zz = fp2_mul(z1, z2);
+    fp2 x;
+    ld_f<fp2>(x, P);
+    u1 = fp2_mul(x, z2z2);
+    ld_f<fp2>(x, Q);
+    h = fp2_sub(fp2_mul(x, z1z1), u1);
+  }
+  if (fp2_is_zero(h)) return false;
+  fp2 s1, rr;
+  {
+    fp2 y;
+    ld_f<fp2>(y, P + 24);
+    s1 = fp2_mul(y, c2);
+    ld_f<fp2>(y, Q + 24);
+    rr = fp2_dbl(fp2_sub(fp2_mul(y, c1), s1));
+  }
+  const fp2 i = fp2_sqr(fp2_dbl(h));
+  const fp2 j = fp2_mul(h, i);
+  const fp2 v = fp2_mul(u1, i);
+  r.x = fp2_sub(fp2_sub(fp2_sqr(rr), j), fp2_dbl(v));
+  r.y = fp2_sub(fp2_mul(rr, fp2_sub(v, r.x)), fp2_dbl(fp2_mul(s1, j)));
+  r.z = fp2_dbl(fp2_mul(zz, h));
+  return true;
+}
+
 // the other group of the pairing
 template <class F>
 struct other;
@@ -107,5 +143,39 @@ DH_DEV jac<fp> g1_gen() { return {fp_c(cst::G1X), fp_c(cst::G1Y), fp_one()}; }
 DH_DEV jac<fp2> g2_gen() { return {fp2_c(cst::G2X), fp2_c(cst::G2Y), fp2_one()}; }
 
 static inline unsigned nblk(size_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+// DigestBeacon of round i; false when the chained record is longer than its slot (a caller error on the
+// device entry point: the round is rejected instead of reading past the record)
+DH_DEV bool beacon_digest(sha_h& d, const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs, size_t prev_stride,
+                          const uint32_t* __restrict__ prev_lens, int chained, size_t i) {
+  if (!chained) {
+    d = digest_unchained(rounds[i]);
+    return true;
+  }
+  const uint64_t pl = prev_lens ? (uint64_t)prev_lens[i] : (uint64_t)prev_stride;
+  if (pl > prev_stride) {
+    d = digest_unchained(rounds[i]);
+    return false;
+  }
+  const uint8_t* p = prevs + i * prev_stride;
+  if (pl <= 96 && (pl & 3) == 0 && (((uintptr_t)p) & 3) == 0) d = digest_chained(p, (uint32_t)pl, rounds[i]);
+  else d = digest_chained_any(p, (uint32_t)pl, rounds[i]);
+  return true;
+}
+
+// message i: the beacon digest of (rounds, prevs) or, for VerifyRecovered / tbls, the given 32-byte msgs32[i]
+DH_DEV sha_h message_of(const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs, size_t prev_stride,
+                        const uint32_t* __restrict__ prev_lens, const uint8_t* __restrict__ msgs32, int chained, size_t i,
+                        uint8_t* __restrict__ status) {
+  sha_h d;
+  if (msgs32) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) d.h[j] = ld_be32a(msgs32 + 32 * i + 4 * j);
+  } else if (!beacon_digest(d, rounds, prevs, prev_stride, prev_lens, chained, i) && status) {
+    status[i] = DEC_BAD;
+  }
+  return d;
+}
+
 
 }  // namespace dh

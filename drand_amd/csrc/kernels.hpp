@@ -46,9 +46,12 @@ inline size_t msm_meta_bytes(size_t max_entries) { return msm_nchunks(max_entrie
 
 hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n, uint8_t* status, uint32_t* sig_aff,
                        uint8_t* rand_out, hipStream_t st);
-hipError_t launch_msg(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
-                      size_t n, int chained, int dst_id, uint32_t* q_out, hipStream_t st);
-hipError_t launch_msg32(int sig_g2, const uint8_t* msgs, size_t n, int dst_id, uint32_t* q_out, hipStream_t st);
+// hash points Q_i (before cofactor clearing) of the beacon digests of (rounds, prevs) or of the given 32-byte
+// msgs32; a chained record longer than its slot marks status[i] = DEC_BAD. tmp: hash_tmp_bytes(sig_g2, n).
+size_t hash_tmp_bytes(int sig_g2, size_t n);
+hipError_t launch_hash(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
+                       const uint8_t* msgs32, size_t n, int chained, int dst_id, uint8_t* status, uint32_t* q_out, uint32_t* tmp,
+                       hipStream_t st);
 hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, hipStream_t st);
 hipError_t launch_decode_key(int key_g2, const uint8_t* pk, uint32_t* key_aff, uint8_t* ok, hipStream_t st);
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t st);
@@ -77,8 +80,10 @@ hipError_t launch_leaf_check_vm(int sig_g2, const uint32_t* entries, size_t m, c
 hipError_t launch_multi_pairing_vm(const uint32_t* P, const uint32_t* Q, size_t n, uint32_t* pairs, uint8_t* live,
                                    uint32_t* f_tmp, uint8_t* pass, hipStream_t st);
 
+// synthetic signer: q_tmp n x 72 words and h_tmp hash_tmp_bytes(1, n) for G2 signatures (unused for G1)
 hipError_t launch_sign(int sig_g2, const uint32_t* sk, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride,
-                       const uint32_t* prev_lens, size_t n, int chained, int dst_id, uint8_t* out, hipStream_t st);
+                       const uint32_t* prev_lens, const uint8_t* msgs32, size_t n, int chained, int dst_id, uint8_t* out,
+                       uint32_t* q_tmp, uint32_t* h_tmp, hipStream_t st);
 hipError_t launch_pubkey(int key_g2, const uint32_t* sk, uint8_t* out, hipStream_t st);
 
 // tbls Recover (k_recover.hip)

@@ -143,6 +143,38 @@ DH_DEV sha_h digest_chained(const uint8_t* prev, uint32_t prevlen, uint64_t roun
   return s;
 }
 
+// DigestBeacon for the chained scheme with a previous signature of ANY length and alignment: the reference
+// hashes whatever the store holds (crypto/schemes.go:106-114, chain/boltdb/trimmed.go:183-189), so a
+// corrupted 31-, 97- or 100-byte record is hashed too and simply fails verification. Byte loads, one
+// compression per 64 bytes; the stored-signature shape (4-byte aligned, <= 96 bytes) takes digest_chained.
+DH_DEV sha_h digest_chained_any(const uint8_t* prev, uint32_t prevlen, uint64_t round) {
+  const uint64_t total = (uint64_t)prevlen + 8;
+  const uint64_t nb = (total + 9 + 63) >> 6;
+  sha_h s = sha_iv();
+#pragma unroll 1
+  for (uint64_t blk = 0; blk < nb; blk++) {
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint64_t pos = blk * 64 + (uint64_t)(4 * j + b);
+        uint32_t byte = 0;
+        if (pos < prevlen) byte = prev[pos];
+        else if (pos < total) byte = (uint32_t)(round >> (8 * (7 - (pos - prevlen)))) & 0xffu;
+        else if (pos == total) byte = 0x80u;
+        v = (v << 8) | byte;
+      }
+      if (blk == nb - 1 && j == 14) v = (uint32_t)((total * 8) >> 32);
+      if (blk == nb - 1 && j == 15) v = (uint32_t)(total * 8);
+      w[j] = v;
+    }
+    sha_compress(s, w);
+  }
+  return s;
+}
+
 // expand_message_xmd(SHA-256, msg = 32-byte digest, DST = 43 bytes, len = 32*NOUT):
 // writes NOUT 32-byte blocks b_1..b_NOUT (as big-endian words) into out[NOUT][8].
 // dst_id 0 = G2 DST, 1 = G1 DST; len_id 0 = 128 bytes (hash to G1), 1 = 256 bytes (G2).

@@ -81,14 +81,22 @@ class Scheme:
     def verify_beacons(self, pubkey, rounds, signatures, previous_signatures=None, seed=0, want_randomness=True):
         """Verify n rounds at once.
 
-        rounds: (n,) uint64; signatures: (n, sig_len) uint8; previous_signatures (chained only):
-        (n, L) uint8 with L a multiple of 4 <= 96, or a list of bytes (lengths may differ).
+        rounds: (n,) uint64; signatures: (n, sig_len) uint8; previous_signatures (chained only): (n, L) uint8 or
+        a list of bytes of any lengths (the reference hashes whatever is stored, crypto/schemes.go:106-114).
         Returns (verdicts (n,) bool, randomness (n, 32) uint8 or None)."""
         rounds = np.ascontiguousarray(rounds, dtype=np.uint64)
         sigs = np.ascontiguousarray(signatures, dtype=np.uint8)
         n = len(rounds)
         if sigs.shape != (n, self.sig_len):
             raise SchemeError("signatures must be (%d, %d)" % (n, self.sig_len))
+        if self.chained and previous_signatures is not None and not isinstance(previous_signatures, np.ndarray):
+            items = [bytes(p or b"") for p in previous_signatures]
+            if len(items) != n:
+                raise SchemeError("previous_signatures must have one entry per round")
+            big = np.array([len(p) > PREV_SLOT_MAX for p in items], dtype=bool)
+            if big.any():
+                return self._verify_with_oversize(pubkey, rounds, sigs, items, big, seed, want_randomness)
+            previous_signatures = items
         prev = plen = None
         pstride = 0
         if self.chained and previous_signatures is not None:
@@ -98,6 +106,26 @@ class Scheme:
         _check(_lib.load().dh_verify_batch(self.id, bytes(pubkey), len(pubkey), _ptr(rounds), _ptr(sigs), self.sig_len,
                                            _ptr(prev), pstride, _ptr(plen), n, _ptr(verdict), _ptr(rand), int(seed)))
         return verdict.astype(bool), rand
+
+    def _verify_with_oversize(self, pubkey, rounds, sigs, items, big, seed, want_randomness):
+        """Rounds whose previous signature exceeds PREV_SLOT_MAX bytes (a corrupted store, never a real chain):
+        VerifyBeacon = VerifyRecovered(pk, DigestBeacon(b), sig) (crypto/schemes.go:70-72), with the digest hashed
+        on the host (dh_digest_batch) and the pairing check on the device; the rest go through the batch path."""
+        n = len(rounds)
+        verdict = np.zeros(n, dtype=bool)
+        rand = np.zeros((n, 32), dtype=np.uint8) if want_randomness else None
+        small = np.flatnonzero(~big)
+        if len(small):
+            v, r = self.verify_beacons(pubkey, rounds[small], sigs[small], [items[i] for i in small], seed, want_randomness)
+            verdict[small] = v
+            if want_randomness:
+                rand[small] = r
+        large = np.flatnonzero(big)
+        msgs = [self.digest_beacon(int(rounds[i]), items[i]) for i in large]
+        verdict[large] = self.verify_recovered_batch(pubkey, msgs, sigs[large], seed=seed)
+        if want_randomness:
+            rand[large] = self.randomness(sigs[large])
+        return verdict, rand
 
     # ---- threshold BLS (kyber sign/tbls as used at chain/beacon/chainstore.go:202,207)
     def verify_recovered(self, pubkey, msg, sig):
@@ -214,27 +242,34 @@ class Scheme:
         return self.name
 
 
+# Previous signatures up to this many bytes travel in one fixed-stride slot array (a stored signature is 96 B);
+# longer records only come from corrupted stores and are verified one digest at a time (_verify_with_oversize).
+PREV_SLOT_MAX = 4096
+
+
 def _pack_prevs(previous_signatures, n):
+    """-> (prevs u8[n, stride], lengths u32[n], stride): any lengths up to the stride; the device hashes exactly
+    lengths[i] bytes of row i."""
     if isinstance(previous_signatures, np.ndarray) and previous_signatures.ndim == 2:
         prev = np.ascontiguousarray(previous_signatures, dtype=np.uint8)
         if len(prev) != n:
             raise SchemeError("previous_signatures must have one row per round")
         width = prev.shape[1]
-        if width % 4 or width > 96:
-            raise SchemeError("previous signature length must be a multiple of 4 and <= 96")
         plen = np.full(n, width, dtype=np.uint32)
-        return prev, plen, max(width, 4)
+        if width == 0:
+            return np.zeros((n, 4), np.uint8), plen, 4
+        return prev, plen, width
     items = [bytes(p or b"") for p in previous_signatures]
     if len(items) != n:
         raise SchemeError("previous_signatures must have one entry per round")
-    prev = np.zeros((n, 96), dtype=np.uint8)
+    longest = max((len(p) for p in items), default=0)
+    stride = max(96, (longest + 3) // 4 * 4)
+    prev = np.zeros((n, stride), dtype=np.uint8)
     plen = np.zeros(n, dtype=np.uint32)
     for i, p in enumerate(items):
-        if len(p) % 4 or len(p) > 96:
-            raise SchemeError("previous signature %d has unsupported length %d" % (i, len(p)))
         prev[i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
         plen[i] = len(p)
-    return prev, plen, 96
+    return prev, plen, stride
 
 
 _SCHEMES = {

@@ -148,7 +148,9 @@ class BoltTrimmedStore(_BoltStoreBase):
     def columns(self, first, last, sig_len):
         """Rounds first..last as (rounds u64[n], sigs u8[n, sig_len], prevs list | None, missing rounds).
         Rounds whose record is missing (or whose previous record is missing, chained) are left out of the
-        columns and returned in `missing`, which is what CheckPastBeacons reports as faulty for them."""
+        columns and returned in `missing`, which is what CheckPastBeacons reports as faulty for them. A stored
+        signature of the wrong length is zero-filled, never cut to a prefix: kilic's UnmarshalBinary rejects
+        any wrong-length point and an all-zero record never decodes, so the round is rejected as in Go."""
         rounds, sigs, prevs, missing = [], [], [], []
         for r in range(int(first), int(last) + 1):
             try:
@@ -158,7 +160,8 @@ class BoltTrimmedStore(_BoltStoreBase):
                 continue
             rounds.append(r)
             s = np.zeros(sig_len, np.uint8)
-            s[:min(sig_len, len(b.signature))] = np.frombuffer(b.signature[:sig_len], np.uint8)
+            if len(b.signature) == sig_len:
+                s[:] = np.frombuffer(b.signature, np.uint8)
             sigs.append(s)
             prevs.append(b.previous_signature)
         sig_arr = np.array(sigs, dtype=np.uint8).reshape(-1, sig_len)

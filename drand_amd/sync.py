@@ -11,6 +11,10 @@ The store model is the bbolt "trimmed" layout (/root/reference/chain/boltdb/trim
 key = round, value = signature; for chained schemes Get(r) rebuilds PreviousSig from the stored signature of
 round r-1 and fails if that one is missing (the genesis "signature" at round 0 is the genesis seed).
 """
+import queue
+import threading
+import time
+
 import numpy as np
 
 from .chain import Beacon
@@ -108,12 +112,38 @@ class WrongBeaconID(Exception):
     pass
 
 
-def sync_from_stream(packets, scheme, pubkey, store, up_to, beacon_id="", window=500, seed=0):
+_END = object()
+
+
+def _packet_queue(packets):
+    """A queue.Queue of the packets (ended by _END): the caller's own queue is used as is (a gRPC receive loop
+    feeding it, the 500-deep channel of net/client_grpc.go:209-212); any other iterable is drained by a daemon
+    reader thread, so the verifier can wait for the next packet with a timeout."""
+    if isinstance(packets, queue.Queue):
+        return packets
+    q = queue.Queue(maxsize=500)
+
+    def reader():
+        try:
+            for p in packets:
+                q.put(p)
+        finally:
+            q.put(_END)
+
+    threading.Thread(target=reader, daemon=True).start()
+    return q
+
+
+def sync_from_stream(packets, scheme, pubkey, store, up_to, beacon_id="", window=500, seed=0, idle=0.05,
+                     max_delay=1.0):
     """tryNode's receive loop (/root/reference/chain/beacon/sync_manager.go:376-445) with verify-ahead windows
-    (SURVEY.md §8f row 4): packets arrive in order; up to `window` of them (the 500-deep gRPC buffer,
-    /root/reference/net/client_grpc.go:209) are verified in one batch, then stored in order until the first
-    packet that has the wrong beacon ID or fails verification (the serial loop stops at that packet, having
-    stored everything before it). Each packet is a dict {round, signature, previous_signature[, beacon_id]}.
+    (SURVEY.md §8f row 4). Packets arrive in order; they are verified in batches of up to `window` (the 500-deep
+    gRPC buffer, /root/reference/net/client_grpc.go:209), and also as soon as the stream goes quiet for `idle`
+    seconds or the oldest waiting packet has waited `max_delay` seconds — a live follow (one beacon per period)
+    stores each beacon right after it arrives instead of waiting for 500 more. After verification, packets are
+    stored in order until the first one that has the wrong beacon ID or fails verification (the serial loop stops
+    at that packet, having stored everything before it). `packets` is an iterable or a queue.Queue of dicts
+    {round, signature, previous_signature[, beacon_id]}, a queue ended by sync.END.
     Returns (done, stored rounds): done = the packet of round `up_to` was stored."""
     stored = []
     buf = []
@@ -142,11 +172,27 @@ def sync_from_stream(packets, scheme, pubkey, store, up_to, beacon_id="", window
         buf.clear()
         return None
 
-    for p in packets:
+    q = _packet_queue(packets)
+    first_at = 0.0
+    while True:
+        timeout = None
+        if buf:
+            timeout = max(0.0, min(idle, first_at + max_delay - time.monotonic()))
+        try:
+            p = q.get(timeout=timeout)
+        except queue.Empty:  # the stream went quiet (or the oldest packet waited long enough): verify now
+            r = drain()
+            if r is not None:
+                return (r, stored)
+            continue
+        if p is _END:
+            break
         bid = p.get("beacon_id")
         if bid is not None and bid != beacon_id:
             r = drain()  # packets before the mismatch were received first and are processed first
             return (bool(r), stored)
+        if not buf:
+            first_at = time.monotonic()
         buf.append(p)
         if len(buf) >= window:
             r = drain()
@@ -154,3 +200,6 @@ def sync_from_stream(packets, scheme, pubkey, store, up_to, beacon_id="", window
                 return (r, stored)
     r = drain()
     return (bool(r), stored)
+
+
+END = _END
