@@ -78,12 +78,13 @@ class Scheme:
             raise SchemeError("bls: invalid signature")
 
     # ---- batch API (new): one call for many rounds sharing the group key
-    def verify_beacons(self, pubkey, rounds, signatures, previous_signatures=None, seed=0, want_randomness=True):
+    def verify_beacons(self, pubkey, rounds, signatures, previous_signatures=None, seed=0, want_randomness=True,
+                       previous_lengths=None):
         """Verify n rounds at once.
 
-        rounds: (n,) uint64; signatures: (n, sig_len) uint8; previous_signatures (chained only): (n, L) uint8 or
-        a list of bytes of any lengths (the reference hashes whatever is stored, crypto/schemes.go:106-114).
-        Returns (verdicts (n,) bool, randomness (n, 32) uint8 or None)."""
+        rounds: (n,) uint64; signatures: (n, sig_len) uint8; previous_signatures (chained only): (n, L) uint8 (row i
+        holds previous_lengths[i] bytes, default L) or a list of bytes of any lengths (the reference hashes whatever
+        is stored, crypto/schemes.go:106-114). Returns (verdicts (n,) bool, randomness (n, 32) uint8 or None)."""
         rounds = np.ascontiguousarray(rounds, dtype=np.uint64)
         sigs = np.ascontiguousarray(signatures, dtype=np.uint8)
         n = len(rounds)
@@ -101,6 +102,10 @@ class Scheme:
         pstride = 0
         if self.chained and previous_signatures is not None:
             prev, plen, pstride = _pack_prevs(previous_signatures, n)
+            if previous_lengths is not None:
+                plen = np.ascontiguousarray(previous_lengths, dtype=np.uint32)
+                if plen.shape != (n,) or (n and int(plen.max()) > pstride):
+                    raise SchemeError("previous_lengths must give one length <= the row width per round")
         verdict = np.zeros(n, dtype=np.uint8)
         rand = np.zeros((n, 32), dtype=np.uint8) if want_randomness else None
         _check(_lib.load().dh_verify_batch(self.id, bytes(pubkey), len(pubkey), _ptr(rounds), _ptr(sigs), self.sig_len,

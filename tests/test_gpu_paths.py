@@ -1,0 +1,374 @@
+"""GPU parity for the round-2 paths, through the C ABI against the CPU oracle (test infrastructure):
+  * chained DigestBeacon over previous signatures of any length (crypto/schemes.go:106-114,
+    chain/boltdb/trimmed.go:183-189) and CheckPastBeacons marking only the affected rounds faulty
+    (chain/beacon/sync_manager.go:215-217);
+  * tbls Recover / VerifyPartial at the BASELINE config shape n = 64, t = 33 (chain/beacon/chainstore.go:202-207);
+  * a real sequential chained replay (prev = stored signature of round-1) with the three Cfg5 corruption
+    classes, faulty set = U{k, k+1} (core/drand_test.go:1105-1111);
+  * concurrent callers (SURVEY.md §8b threading contract) and one-call multi-stream splitting;
+  * the stream-sync micro-batcher on the device (chain/beacon/sync_manager.go:376-445).
+"""
+import hashlib
+import json
+import os
+import queue
+import random
+import subprocess
+import sys
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "bench"))
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+R_ORDER = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+CHAINED = "pedersen-bls-chained"
+
+
+@pytest.fixture(scope="module")
+def dh():
+    import drand_amd
+    from drand_amd import _lib
+    assert _lib.load().dh_init(0) == 0, _lib.last_error()
+    return drand_amd
+
+
+def _secret(tag):
+    return (int.from_bytes(hashlib.sha256(tag).digest(), "big") % R_ORDER).to_bytes(32, "big")
+
+
+# ---------------------------------------------------------------- chained digests of any length
+def test_chained_prev_any_length(dh, oracle):
+    """Previous signatures of 0/1/4/31/32/95/96/97/100/300 and 5000 bytes: the device hashes exactly what it is
+    given (valid when the round was signed over that record, invalid otherwise), matching the oracle per round."""
+    s = dh.scheme_from_name(CHAINED)
+    sk = _secret(b"anylen")
+    pk = s.public_key(sk)
+    rng = np.random.default_rng(3)
+    lengths = [0, 1, 4, 31, 32, 95, 96, 97, 100, 300, 5000]
+    rounds = np.arange(1000, 1000 + 2 * len(lengths), dtype=np.uint64)
+    prevs = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lengths for _ in range(2)]
+    signed_over = list(prevs)
+    for k in range(1, len(prevs), 2):  # every second round was signed over a different record
+        signed_over[k] = prevs[k][:-1] + bytes([prevs[k][-1] ^ 1]) if prevs[k] else b"\x00" * 7
+    small = [k for k in range(len(prevs)) if len(signed_over[k]) <= 4096]
+    sigs = np.zeros((len(rounds), 96), np.uint8)
+    sigs[small] = s.sign_beacons(sk, rounds[small], [signed_over[k] for k in small])
+    for k in range(len(prevs)):
+        want_sig = oracle.sign(CHAINED, sk, oracle.digest_beacon(CHAINED, int(rounds[k]), signed_over[k]))
+        if k in small:  # the device signer hashes odd-length records exactly as the oracle does
+            assert sigs[k].tobytes() == want_sig, k
+        else:
+            sigs[k] = np.frombuffer(want_sig, np.uint8)
+    v, rand = s.verify_beacons(pk, rounds, sigs, prevs, seed=21)
+    want = [oracle.verify_beacon(CHAINED, pk, int(r), sigs[k].tobytes(), prevs[k]) for k, r in enumerate(rounds)]
+    assert v.tolist() == want
+    assert want == [k % 2 == 0 for k in range(len(prevs))]
+    assert rand[5].tobytes() == hashlib.sha256(sigs[5].tobytes()).digest()
+    for k in (2, 3, 16):  # single-beacon path
+        b = dh.Beacon(int(rounds[k]), sigs[k].tobytes(), prevs[k])
+        if want[k]:
+            s.verify_beacon(b, pk)
+        else:
+            with pytest.raises(dh.SchemeError):
+                s.verify_beacon(b, pk)
+
+
+def _serial_check(oracle, pk, sig_of, n, up_to):
+    """CheckPastBeacons (chain/beacon/sync_manager.go:191-225) serially on the oracle over a trimmed store."""
+    faulty = []
+    for r in range(1, n):
+        sig, prev = sig_of.get(r), sig_of.get(r - 1)
+        if sig is None or prev is None:
+            faulty.append(r)
+        elif len(sig) != 96 or not oracle.verify_beacon(CHAINED, pk, r, sig, prev):
+            faulty.append(r)
+        if r >= up_to:
+            break
+    return faulty
+
+
+def test_check_past_beacons_odd_records(dh, oracle):
+    """A trimmed store whose records at some rounds are 0/31/95/97/100 bytes: CheckPastBeacons reports exactly
+    the oracle's faulty rounds (the odd record's round and the next one, whose previous signature is that record)
+    instead of aborting the window."""
+    from drand_amd.sync import TrimmedMemStore, check_past_beacons
+    c = json.load(open(os.path.join(GOLD, "chains.json")))[CHAINED]
+    s = dh.scheme_from_name(CHAINED)
+    pk = bytes.fromhex(c["pk"])
+    st = TrimmedMemStore(True)
+    sig_of = {0: bytes.fromhex(c["prevs"][0])}
+    for r, sig in zip(c["rounds"], c["sigs"]):
+        sig_of[r] = bytes.fromhex(sig)
+    rng = random.Random(9)
+    for r, L in zip((3, 7, 11, 15, 19), (0, 31, 95, 97, 100)):
+        sig_of[r] = bytes(rng.randrange(256) for _ in range(L))
+    for r, sig in sig_of.items():
+        st.put(r, sig)
+    n = st.len()
+    got = check_past_beacons(st, s, pk, 1000, window=9)
+    assert got == _serial_check(oracle, pk, sig_of, n, 1000)
+    assert got == [3, 4, 7, 8, 11, 12, 15, 16, 19, 20]
+
+
+# ---------------------------------------------------------------- tbls at n = 64, t = 33
+def _dealer(s, t, tag):
+    coeffs = [int.from_bytes(hashlib.sha256(b"%s-%d" % (tag, j)).digest(), "big") % R_ORDER for j in range(t)]
+    commits = [s.public_key(cf.to_bytes(32, "big")) for cf in coeffs]
+    return coeffs, commits
+
+
+def _share(coeffs, i):
+    x, acc = i + 1, 0
+    for cf in reversed(coeffs):
+        acc = (acc * x + cf) % R_ORDER
+    return acc.to_bytes(32, "big")
+
+
+def test_recover_config4_n64_t33(dh, oracle):
+    """chain/beacon/chainstore.go:202-207 at the BASELINE shape: 64 signers, threshold 33, 160 rounds with random
+    signer subsets in random arrival order, invalid partials (another round's signature, a flipped bit), duplicate
+    indices, an index outside the group, and rounds with fewer than t valid partials. Recover bytes + status and
+    VerifyPartial per partial are compared with the oracle (kyber sign/tbls restated)."""
+    s = dh.scheme_from_name("pedersen-bls-unchained")
+    n, t, nr = 64, 33, 160
+    coeffs, commits = _dealer(s, t, b"cfg4")
+    rounds = np.arange(7000, 7000 + nr, dtype=np.uint64)
+    shares = [s.sign_beacons(_share(coeffs, i), rounds) for i in range(n)]
+    msgs = [s.digest_beacon(int(r)) for r in rounds]
+    rng = random.Random(2024)
+    parts = []
+    for j in range(nr):
+        kind = j % 8
+        k = rng.randrange(t - 3, t) if kind == 7 else rng.randrange(t, n + 1)  # kind 7: fewer than t signers
+        ids = rng.sample(range(n), k)
+        ps = [i.to_bytes(2, "big") + shares[i][j].tobytes() for i in ids]
+        if kind in (1, 4):  # invalid partials in front: another round's signature, a flipped bit
+            i = ids[0]
+            ps.insert(0, i.to_bytes(2, "big") + shares[i][(j + 1) % nr].tobytes())
+            bad = bytearray(ps[-1])
+            bad[40] ^= 0x08
+            ps.insert(1, bytes(bad))
+        if kind == 2:  # duplicate index (same partial twice) early in the arrival order
+            ps.insert(3, ps[0])
+        if kind == 3:  # an index outside the group (kyber evaluates any index; node.go:138-141 filters them)
+            ps.insert(0, (n + 6).to_bytes(2, "big") + shares[5][j].tobytes())
+        rng.shuffle(ps) if kind == 5 else None
+        parts.append(ps)
+    sigs, ok = s.recover_batch(commits, t, n, msgs, parts)
+
+    def oracle_round(j):
+        return oracle.recover(s.name, commits, t, n, msgs[j], parts[j])
+
+    with ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(oracle_round, range(nr)))
+    for j in range(nr):
+        assert bool(ok[j]) == (want[j] is not None), j
+        if want[j] is not None:
+            assert sigs[j].tobytes() == want[j], j
+    assert ok.sum() >= nr * 3 // 4 and not ok.all()
+    group_sig = s.sign_beacons(coeffs[0].to_bytes(32, "big"), rounds)
+    assert np.array_equal(sigs[ok], group_sig[ok])  # the property pin: [f(0)] H(m)
+    # VerifyPartial per partial on a subset of rounds (each oracle check is a full pairing)
+    sub = list(range(0, nr, 5))  # every kind of round (j % 8) appears
+    got = s.verify_partials_batch(commits, t, n, [msgs[j] for j in sub], [parts[j] for j in sub])
+    evals = {}
+
+    def oracle_partial(jk):
+        j, p = jk
+        i = s.index_of(p)
+        if i >= n:
+            return False  # documented: indices outside the group are rejected (include/drandhip.h)
+        if i not in evals:
+            evals[i] = oracle.pubpoly_eval(s.name, commits, i)
+        return oracle.verify(s.name, evals[i], msgs[j], p[2:])
+
+    jobs = [(j, p) for j in sub for p in parts[j]]
+    with ThreadPoolExecutor(16) as ex:
+        want_p = list(ex.map(oracle_partial, jobs))
+    flat = [bool(x) for g in got for x in g]
+    assert flat == want_p
+    assert not all(want_p)
+
+
+def test_recover_mostly_empty_rounds(dh):
+    """1000 rounds of which only 3 have t partials (most have none or fewer than t): the VerifyRecovered batch over
+    all rounds must size its scalars for the rounds, not the partials (r_scal overflow)."""
+    s = dh.scheme_from_name("bls-unchained-g1-rfc9380")
+    n, t, nr = 7, 4, 1000
+    coeffs, commits = _dealer(s, t, b"sparse")
+    rounds = np.arange(1, nr + 1, dtype=np.uint64)
+    good = {17, 500, 999}
+    shares = {i: s.sign_beacons(_share(coeffs, i), rounds[sorted(good)]) for i in range(n)}
+    msgs = [s.digest_beacon(int(r)) for r in rounds]
+    parts = []
+    for j in range(nr):
+        if j in good:
+            g = sorted(good).index(j)
+            parts.append([i.to_bytes(2, "big") + shares[i][g].tobytes() for i in (6, 1, 3, 0, 2)])
+        elif j % 3 == 0:
+            parts.append([i.to_bytes(2, "big") + shares[i][0].tobytes() for i in (0, 1)])
+        else:
+            parts.append([])
+    sigs, ok = s.recover_batch(commits, t, n, msgs, parts)
+    assert np.flatnonzero(ok).tolist() == sorted(good)
+    want = s.sign_beacons(coeffs[0].to_bytes(32, "big"), rounds[sorted(good)])
+    assert np.array_equal(sigs[sorted(good)], want)
+
+
+# ---------------------------------------------------------------- real sequential chained replay (Cfg5 shape)
+def test_chained_replay_real_chain(dh, oracle):
+    """16 384 rounds of a sequential chain (each round signed over the stored signature of the round before,
+    genesis seed for round 1), 1% of the rounds corrupted in the three Cfg5 classes (sigma + g2, a flipped bit, an
+    on-curve point outside the subgroup): the batch replay rejects exactly U{k, k+1}, which the oracle confirms on
+    every faulty round and a sample of the valid ones; check_past_beacons over the store reports the same rounds."""
+    import chainsynth
+    from drand_amd.sync import TrimmedMemStore, check_past_beacons
+    s = dh.scheme_from_name(CHAINED)
+    sk = _secret(b"drandhip-sk-" + CHAINED.encode())
+    pk = s.public_key(sk)
+    n = 1 << 14
+    genesis = hashlib.sha256(b"drandhip-genesis").digest()
+    bad = chainsynth.corrupted_rounds(n, n // 100)
+    rng = np.random.default_rng(0xC5)
+    t0 = time.time()
+    sigs = chainsynth.sign_chain(s, sk, 1, n, genesis, bad, rng)
+    t_sign = time.time() - t0
+    prev, plen = chainsynth.stored_prevs(sigs, genesis)
+    rounds = np.arange(1, n + 1, dtype=np.uint64)
+    v, _ = s.verify_beacons(pk, rounds, sigs, prev, seed=77, previous_lengths=plen)
+    heads = sorted(int(k) + 1 for k in bad if k + 1 < n)  # segment heads: signed over a stand-in for sigma_k
+    assert np.flatnonzero(~v).tolist() == heads  # every other round is a verified link of the chain
+    prng = random.Random(31)
+    chainsynth.corrupt(sigs, bad, prng)
+    prev, plen = chainsynth.stored_prevs(sigs, genesis)
+    v, _ = s.verify_beacons(pk, rounds, sigs, [prev[i, :plen[i]].tobytes() for i in range(n)], seed=78)
+    expected = chainsynth.expected_faulty(bad, n)
+    assert np.flatnonzero(~v).tolist() == expected.tolist()
+    # oracle: every rejected round and 1500 sampled accepted rounds
+    sample = np.sort(np.concatenate([expected, np.random.default_rng(1).choice(n, 1500, replace=False)]))
+    sample = np.unique(sample)
+    ov = np.zeros(len(sample), np.uint8)
+    import ctypes
+    lib = oracle.lib()
+    rs = np.ascontiguousarray(rounds[sample])
+    ss = np.ascontiguousarray(sigs[sample])
+    ps = np.ascontiguousarray(prev[sample])
+    ls = np.ascontiguousarray(plen[sample])
+    lib.or_verify_batch(oracle.sid(CHAINED), pk, len(pk), rs.ctypes.data, ss.ctypes.data, 96, ps.ctypes.data, 96,
+                        ls.ctypes.data, len(sample), 16, ov.ctypes.data, None)
+    assert ov.astype(bool).tolist() == v[sample].tolist()
+    st = TrimmedMemStore(True)
+    st.put(0, genesis)
+    for i in range(n):
+        st.put(i + 1, sigs[i].tobytes())
+    assert check_past_beacons(st, s, pk, n) == (expected + 1).tolist()
+    print("chain of %d rounds signed in %.1f s" % (n, t_sign))
+
+
+# ---------------------------------------------------------------- threading contract
+def test_concurrent_callers(dh):
+    """8 threads call the C ABI at once on mixed schemes (batch verify, single verify, Recover, VerifyPartial), one
+    of them calling dh_shutdown midway (leased workers are retired, not freed under a running call); every result
+    matches the golden fixtures."""
+    from drand_amd import _lib
+    chains = json.load(open(os.path.join(GOLD, "chains.json")))
+    neg = json.load(open(os.path.join(GOLD, "negatives.json")))
+    rec = json.load(open(os.path.join(GOLD, "recover.json")))["pedersen-bls-unchained"]
+    errors = []
+
+    def job(tid):
+        try:
+            for it in range(4):
+                name = list(chains)[(tid + it) % 4]
+                c = chains[name]
+                s = dh.scheme_from_name(name)
+                sigs = np.array([np.frombuffer(bytes.fromhex(x), np.uint8) for x in c["sigs"]])
+                prevs = [bytes.fromhex(p) for p in c["prevs"]] if s.chained else None
+                v, rand = s.verify_beacons(bytes.fromhex(c["pk"]), c["rounds"], sigs, prevs, seed=tid + 1)
+                assert v.tolist() == c["valid"] and [r.tobytes().hex() for r in rand] == c["randomness"]
+                cases = neg[name]["cases"]
+                sg = np.array([np.frombuffer(bytes.fromhex(x["sig"]), np.uint8) for x in cases])
+                pv = [bytes.fromhex(x["prev"]) for x in cases] if s.chained else None
+                v2, _ = s.verify_beacons(bytes.fromhex(neg[name]["pk"]), [x["round"] for x in cases], sg, pv)
+                assert v2.tolist() == [x["valid"] for x in cases]
+                if tid % 2 == 0:
+                    rs = dh.scheme_from_name("pedersen-bls-unchained")
+                    commits = [bytes.fromhex(x) for x in rec["commits"]]
+                    msgs = [bytes.fromhex(x["msg"]) for x in rec["cases"]]
+                    parts = [[bytes.fromhex(p) for p in x["partials"]] for x in rec["cases"]]
+                    got, ok = rs.recover_batch(commits, rec["t"], rec["n"], msgs, parts)
+                    for k, x in enumerate(rec["cases"]):
+                        assert bool(ok[k]) == (x["expected"] is not None)
+                        if x["expected"]:
+                            assert got[k].tobytes().hex() == x["expected"]
+                if tid == 3 and it == 1:
+                    _lib.load().dh_shutdown()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((tid, repr(e)))
+
+    ths = [threading.Thread(target=job, args=(t,)) for t in range(8)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=240)
+    assert not errors, errors
+    assert _lib.load().dh_init(0) == 0
+
+
+def test_single_call_split():
+    """One dh_verify_batch / dh_verify_batch_device call over 60 000 quicknet rounds, split by the library over
+    4 internal streams in 6 000-round chunks (DRANDHIP_SPLIT), with corrupted rounds in several chunks: verdicts,
+    randomness and stats are those of the unsplit call."""
+    env = dict(os.environ, DRANDHIP_SPLIT="6000,4")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "split_check.py")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    assert got["rejected"] == got["expected"] and got["device_rejected"] == got["expected"]
+    assert got["rand_ok"] and got["stats"][3] == len(got["expected"])
+
+
+# ---------------------------------------------------------------- stream sync on the device
+def test_sync_from_stream_device(dh):
+    """tryNode's receive loop (chain/beacon/sync_manager.go:376-445) over a live queue: packets that arrive and then
+    a quiet stream are verified and stored without waiting for a full window; an invalid packet stops the peer
+    after everything before it is stored."""
+    from drand_amd.sync import END, TrimmedMemStore, sync_from_stream
+    c = json.load(open(os.path.join(GOLD, "chains.json")))[CHAINED]
+    s = dh.scheme_from_name(CHAINED)
+    pk = bytes.fromhex(c["pk"])
+    pkts = [{"round": r, "signature": bytes.fromhex(x), "previous_signature": bytes.fromhex(p)}
+            for r, x, p in zip(c["rounds"], c["sigs"], c["prevs"])]
+    q = queue.Queue()
+    st = TrimmedMemStore(True)
+    out = {}
+    th = threading.Thread(target=lambda: out.update(res=sync_from_stream(q, s, pk, st, up_to=20, window=500,
+                                                                         idle=0.05, max_delay=0.5)))
+    th.start()
+    for p in pkts[:5]:
+        q.put(p)
+    deadline = time.time() + 60
+    while st.len() < 5 and time.time() < deadline:  # the live follow stores them with the window far from full
+        time.sleep(0.02)
+    assert st.len() == 5
+    for p in pkts[5:]:
+        q.put(p)
+    q.put(END)
+    th.join(timeout=120)
+    done, stored = out["res"]
+    assert done and stored == list(range(1, 21))
+    bad = [dict(p) for p in pkts]
+    bad[12]["signature"] = bad[13]["signature"]
+    q2 = queue.Queue()
+    for p in bad:
+        q2.put(p)
+    q2.put(END)
+    done, stored = sync_from_stream(q2, s, pk, TrimmedMemStore(True), up_to=24, window=8)
+    assert not done and stored == list(range(1, 13))
