@@ -1,20 +1,24 @@
 #!/usr/bin/env python3
 """bench.py — verified beacons/sec on MI355X for the quicknet scheme (bls-unchained-g1-rfc9380).
 
-Workload (BASELINE.json configs[1]): batch-verify 1M synthetic quicknet rounds per GPU — G1 signatures,
-G2 group key, RFC 9380 hash-to-G1 — with per-round verdicts and SHA-256 randomness, inputs resident in
-HBM before the timed region. One "step" = one dh_verify_batch_device call over the GPU's 1M rounds (fresh
-CSPRNG seed each step), followed, for N > 1, by an all-gather of the per-GPU verdict bitmaps over RCCL.
-Rounds shard across GPUs (rank r owns rounds r*n+1 .. (r+1)*n): weak scaling, no data-path collective.
+Workload (BASELINE.json configs[1] and the north_star's "1M-round quicknet chain"): batch-verify a 1M-round synthetic
+quicknet chain — G1 signatures, G2 group key, RFC 9380 hash-to-G1 — with per-round verdicts and SHA-256 randomness,
+inputs resident in HBM before the timed region. Strong scaling by default: the 1M rounds are split across the N
+GPUs of the node (rank r owns a contiguous shard), so N=8 is the north_star's 8xMI355X on a 1M-round chain;
+--rounds-per-gpu gives weak scaling instead. One "step" = every rank verifies its shard once (one library call,
+fresh CSPRNG seed); with N > 1 each call runs under the node-wide check: the ranks' level-0 RLC sums are
+all-gathered over RCCL and ONE pairing check covers the node (drand_amd/dist.py). The verdict
+bitmaps are all-gathered at the end of the timed steps.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rounds n] [--scheme name]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--total-rounds n | --rounds-per-gpu n] [--scheme name]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0 (contract in the task statement): value = rounds verified by all ranks /
-max-over-ranks wall time of the K timed steps. "roofline" reports the dominant kernel's achieved
-integer-multiply rate (algorithmic work of bench/workmodel.json / its HIP-event-measured duration on its
-own stream) against the measured v_mad_u64_u32 peak. "cpu_baseline" times the CPU oracle (a C port of
-the reference's per-round algorithm, oracle/bls_oracle.c) on a bounded sample on the host cores.
+Rank 0 prints ONE JSON line: value = rounds verified by all ranks / max-over-ranks wall time of the K steps.
+"roofline": the dominant kernel's integer-multiply rate (its algorithmic mul32 per launch, bench/workmodel.json, over
+its HIP-event duration on its own stream) against the measured v_mad_u64_u32 peak (bench/microbench_mul.hip).
+"cpu_baseline": the CPU oracle (a C restatement of the reference's per-round VerifyBeacon, oracle/bls_oracle.c) on a
+bounded sample, on the host cores this process may use. "single_call": one dh_verify_batch_device call at a time
+(the drop-in callers' shape), split by the library over its internal streams.
 """
 import argparse
 import ctypes
@@ -22,12 +26,14 @@ import hashlib
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+R_ORDER = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
 
 
 def parse():
@@ -35,19 +41,24 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--rounds", type=int, default=1 << 20, help="rounds per GPU per step")
+    ap.add_argument("--total-rounds", type=int, default=1 << 20, help="strong scaling: rounds split over the GPUs")
+    ap.add_argument("--rounds-per-gpu", type=int, default=0, help="weak scaling: rounds per GPU (overrides)")
     ap.add_argument("--scheme", default="bls-unchained-g1-rfc9380")
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-times", action="store_true",
                     help="leave the library's HIP-event stage timing off inside the timed region")
     ap.add_argument("--roofline-steps", type=int, default=2, help="single-stream batches timed for the roofline")
+    ap.add_argument("--single-call-steps", type=int, default=4, help="one-call-at-a-time batches timed after")
     ap.add_argument("--streams", type=int, default=8,
                     help="batches in flight per GPU (host threads, each with its own HIP stream in libdrandhip)")
     ap.add_argument("--split", default="0",
-                    help="DRANDHIP_SPLIT for the timed calls ('chunk,workers'; 0 = each call on one stream: the bench "
-                         "already keeps --streams calls in flight)")
+                    help="one-call split inside the timed region ('chunk,workers'; 0 = each call on one stream: "
+                         "the bench already keeps --streams calls in flight)")
+    ap.add_argument("--node-check", choices=["auto", "on", "off"], default="auto",
+                    help="node-wide RLC check with an all-gather of partial sums (auto: when N > 1)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="gloo: rehearse N ranks on one GPU with host-staged collectives")
     return ap.parse_args()
 
 
@@ -56,25 +67,46 @@ def load_workmodel():
         return json.load(f)
 
 
-def cpu_baseline(scheme, pk, rounds, sigs, seconds, threads):
-    """Oracle (port of the reference per-round VerifyBeacon) on `threads` host threads, bounded sample."""
+def host_cores():
+    """Threads this process may really run: the CPU affinity mask, capped by the cgroup CPU quota (the GPU box
+    shows the whole machine's CPUs but grants a share of them); plus the CPU model."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return (min(n, quota) if quota else n), n, quota, model
+
+
+def cpu_baseline(scheme, pk, rounds, sigs, seconds):
+    """Oracle (C restatement of the reference per-round VerifyBeacon) on the usable host cores, bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as orc
-    lib = orc.lib()
+    threads, affinity, quota, model = host_cores()
     probe = max(threads, 16)
     t0 = time.perf_counter()
-    v, _ = orc.verify_batch(scheme, pk, rounds[:probe], sigs[:probe], nthreads=threads)
-    dt = time.perf_counter() - t0
-    per = dt / probe
+    orc.verify_batch(scheme, pk, rounds[:probe], sigs[:probe], nthreads=threads)
+    per = (time.perf_counter() - t0) / probe
     n = int(min(len(rounds), max(probe, seconds / max(per, 1e-9))))
     t0 = time.perf_counter()
     v, _ = orc.verify_batch(scheme, pk, rounds[:n], sigs[:n], nthreads=threads)
     dt = time.perf_counter() - t0
     assert v.all(), "oracle rejected a valid synthetic round"
-    del lib
-    return {"value": n / dt, "unit": "beacons/s", "cores": threads, "kind": "port",
-            "sample": "%d quicknet rounds (first of the 1M synthetic chain), per-round decode+subgroup(r*P)+hash+"
-                      "2-pairing VerifyBeacon, %d threads, %.1f s" % (n, threads, dt)}
+    return {"value": round(n / dt, 1), "unit": "beacons/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "sample": "%d quicknet rounds (the first of the synthetic chain): per-round decode + subgroup (r*P) + "
+                      "hash + 2-pairing VerifyBeacon (CPU restatement, not kyber), %d threads, %.1f s" % (n, threads, dt)}
 
 
 def main():
@@ -82,27 +114,38 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    os.environ["DRANDHIP_SPLIT"] = args.split  # read once, when the library first splits a call
+    os.environ["DRANDHIP_SPLIT"] = args.split  # the library's default one-call split, read when it loads
     import torch
     import torch.distributed as dist
     from drand_amd import _lib, scheme_from_name
-    from drand_amd.dist import gather_verdicts, pack_bits, shard_rounds
+    from drand_amd.dist import gather_verdicts, pack_bits, shard_rounds, strong_shard, verify_node_batch
 
+    gloo = args.backend == "gloo"
+    dev_index = 0 if gloo else local  # gloo rehearsal: every rank on GPU 0
     lib = _lib.load()
-    rc = lib.dh_init(1 << local)
+    rc = lib.dh_init(1 << dev_index)
     if rc != 0:
         raise SystemExit("dh_init failed: %s" % _lib.last_error())
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    node_check = args.node_check == "on" or (args.node_check == "auto" and world > 1)
 
     sch = scheme_from_name(args.scheme)
-    n = args.rounds
-    sk = (int.from_bytes(hashlib.sha256(b"drandhip-sk-" + args.scheme.encode()).digest(), "big") %
-          0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001).to_bytes(32, "big")
+    weak = args.rounds_per_gpu > 0
+    if weak:
+        rounds = shard_rounds(rank, world, args.rounds_per_gpu)
+        total = world * args.rounds_per_gpu
+    else:
+        rounds = strong_shard(rank, world, args.total_rounds)
+        total = args.total_rounds
+    n = len(rounds)
+    sk = (int.from_bytes(hashlib.sha256(b"drandhip-sk-" + args.scheme.encode()).digest(), "big") % R_ORDER).to_bytes(32, "big")
     pk = sch.public_key(sk)
-    rounds = shard_rounds(rank, world, n)
     t0 = time.perf_counter()
     sigs = sch.sign_beacons(sk, rounds)  # synthetic chain, signed on the GPU (not timed)
     t_sign = time.perf_counter() - t0
@@ -112,9 +155,18 @@ def main():
     S = max(1, args.streams)
     d_verdict = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(S)]
     d_rand = [torch.zeros((n, 32), dtype=torch.uint8, device=dev) for _ in range(S)]
+    pbytes = lib.dh_partial_bytes(sch.id)
+    d_part = [torch.zeros(pbytes, dtype=torch.uint8, device=dev) for _ in range(S)]
+    # one process group per in-flight slot: slot t on every rank issues its collectives in the same order
+    groups = [dist.new_group(list(range(world))) for _ in range(S)] if world > 1 and node_check else [None] * S
     torch.cuda.synchronize()
+    state = {"node_check": node_check}
 
     def verify(slot):
+        if state["node_check"]:
+            verify_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot], d_rand[slot], d_part[slot], world,
+                              groups[slot], stage_host=gloo)
+            return
         rc = lib.dh_verify_batch_device(sch.id, pk, len(pk), ctypes.c_void_p(d_rounds.data_ptr()),
                                         ctypes.c_void_p(d_sigs.data_ptr()), sch.sig_len, None, 0, None, n,
                                         ctypes.c_void_p(d_verdict[slot].data_ptr()),
@@ -122,15 +174,14 @@ def main():
         if rc != 0:
             raise RuntimeError("dh_verify_batch_device: %s" % _lib.last_error())
 
-    def run_steps(k_steps, streams):
+    def run_steps(k_steps, streams, gather=True):
         """k_steps batches, `streams` in flight: thread t runs steps t, t+streams, ... on its own output slot."""
-        import threading
         errs = []
         bits = [None] * k_steps
 
         def worker(t):
             try:
-                torch.cuda.set_device(local)
+                torch.cuda.set_device(dev_index)
                 for k in range(t, k_steps, streams):
                     verify(t)
                     bits[k] = pack_bits(d_verdict[t])
@@ -144,8 +195,9 @@ def main():
             th.join()
         if errs:
             raise errs[0]
-        if world > 1:  # whole-node verdict bitmaps: one all-gather over RCCL at the end of the batches
-            gather_verdicts(torch.cat(bits), world)
+        if world > 1 and gather and k_steps:  # whole-node verdict bitmaps: one all-gather after the batches
+            b = torch.cat(bits)
+            gather_verdicts(b.cpu() if gloo else b, world)
         torch.cuda.synchronize()
 
     def profile_read():
@@ -168,23 +220,36 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     prof = profile_read()
-    # Roofline pass (after the timed region, not counted in `value`): with S batches in flight the kernels of
-    # different batches share the CUs, so per-launch durations measured there are not one kernel's speed.
-    # Two more batches on ONE stream give each kernel the whole GPU; the dominant kernel's roofline is
-    # computed from their HIP events (recorded on the library's stream). bench/profile.sh collects the
-    # rocprofv3 kernel-trace of the same single-stream batches.
-    lib.dh_profile(1)
-    run_steps(args.roofline_steps, 1)
-    prof1 = profile_read()
-    lib.dh_profile(0)
-
     # sanity (outside the timed region): every synthetic round verifies, randomness = SHA-256(sig)
     ok = all(bool(d.cpu().numpy().all()) for d in d_verdict[:min(S, args.steps)])
     r0 = d_rand[0].cpu().numpy()[0].tobytes()
     ok = ok and r0 == hashlib.sha256(sigs[0].tobytes()).digest()
 
+    # Roofline pass (after the timed region, not counted in `value`): with S batches in flight the kernels of
+    # different batches share the CUs, so per-launch durations there are not one kernel's speed. Single-stream
+    # local batches give each kernel the whole GPU; the dominant kernel's roofline comes from their HIP events (on
+    # the library's stream). bench/profile.sh records the rocprofv3 kernel trace of the same batches.
+    state["node_check"] = False
+    prof1 = {}
+    if args.roofline_steps:
+        lib.dh_profile(1)
+        run_steps(args.roofline_steps, 1, gather=False)
+        prof1 = profile_read()
+        lib.dh_profile(0)
+    single = None
+    if args.single_call_steps and world == 1:  # the drop-in shape: ONE call at a time, split internally
+        lib.dh_set_split(262144, 8)
+        run_steps(1, 1, gather=False)  # warm the split workers
+        t1 = time.perf_counter()
+        run_steps(args.single_call_steps, 1, gather=False)
+        dt = time.perf_counter() - t1
+        single = {"value": round(n * args.single_call_steps / dt, 1), "unit": "beacons/s",
+                  "ms_per_call": round(dt * 1000 / args.single_call_steps, 3), "split": "262144 rounds x 8 streams",
+                  "calls": args.single_call_steps}
+        lib.dh_set_split(0, 1)
+
     if world > 1:
-        t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device="cpu" if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, bad = float(t[0]), float(t[1])
         ok = bad == 0.0
@@ -194,46 +259,52 @@ def main():
 
     wm = load_workmodel()
     ms_per_step = elapsed * 1000.0 / args.steps
-    value = world * n * args.steps / elapsed
+    value = total * args.steps / elapsed
     peak = wm["peak_mul32_per_s_measured"]
-    kern = {k: v for k, v in prof1.items() if k.startswith("k_prep")}
+    units = wm["kernel_units_M_per_round"]
+    kern = {k: v for k, v in prof1.items() if k in units}
     dom = max(kern, key=lambda k: kern[k]["total_ms"]) if kern else None
     roof = None
     if dom:
         avg_s = kern[dom]["total_ms"] / kern[dom]["count"] / 1000.0
-        units = wm["kernel_units_M_per_round"][dom] * wm["mul32_per_M"] * n
-        achieved = units / avg_s / 1e12
+        achieved = units[dom] * wm["mul32_per_M"] * n / avg_s
         traffic = None  # HBM bytes per launch from the committed PMC passes (bench/profile.sh, pmc_summary.py)
-        pmc = os.path.join(ROOT, "profiles", "pmc_r01.json")
+        pmc = os.path.join(ROOT, "profiles", wm.get("pmc_file", "pmc_r02.json"))
         if os.path.exists(pmc):
             per_round = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_round")
             traffic = round(per_round * n) if per_round is not None else None
-        roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved, 3), "peak": round(peak / 1e12, 3),
-                "unit": "Tmul32/s", "frac": round(achieved * 1e12 / peak, 4), "traffic": traffic,
-                "traffic_unit": "bytes per launch (FETCH+WRITE, PMC)",
+        roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved / 1e12, 3), "peak": round(peak / 1e12, 3),
+                "unit": "Tmul32/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE, PMC, uncorrected)",
                 "avg_launch_ms": round(avg_s * 1000, 3),
-                "work_per_launch": "%d M x %d mul32 x %d rounds" % (wm["kernel_units_M_per_round"][dom],
-                                                                   wm["mul32_per_M"], n),
+                "work_per_launch": "%d M x %d mul32 x %d rounds" % (units[dom], wm["mul32_per_M"], n),
+                "peak_source": wm["peak_source"],
                 "measured": "HIP events, %d single-stream batches after the timed region" % args.roofline_steps}
-    w_beacon = wm["W_M_per_beacon"]["g2_sig" if sch.sig_len == 96 else "g1_sig"] * wm["mul32_per_M"]
+    ex_key = "g2_sig" if sch.sig_len == 96 else "g1_sig"
+    executed = wm["executed_M_per_beacon"][ex_key] * wm["mul32_per_M"]
     out = {
         "metric": "verified beacons/sec (whole node), quicknet G1 scheme" if sch.id == 3 else
                   "verified beacons/sec (whole node), %s" % sch.name,
         "value": round(value, 1), "unit": "beacons/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u32 (12x32-bit Montgomery limbs)", "data": "synthetic (GPU-signed chain, seeded key)",
-        "config": {"workload": "%s batch verify, %d rounds per GPU per step" % (sch.name, n), "scheme": sch.name,
-                   "rounds_per_gpu": n, "global_batch": world * n, "parallelism": "round-shard x%d" % world},
+        "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak" if weak else "strong",
+        "vs_baseline": None, "dtype": "u32 (12x32-bit Montgomery limbs)", "data": "synthetic (GPU-signed chain, seeded key)",
+        "config": {"workload": "%s batch verify of a %d-round chain, %s" % (
+                       sch.name, total, "%d rounds per GPU" % n if weak else "split over %d GPU(s)" % world),
+                   "scheme": sch.name, "rounds_total": total, "rounds_per_gpu": n, "global_batch": total,
+                   "parallelism": "round-shard x%d%s" % (world, ", node-wide RLC check (RCCL all-gather)" if node_check else "")},
         "roofline": roof,
-        "node_roofline_frac": round(value * w_beacon / (peak * world), 4),
+        "node_roofline_frac": round(value * executed / (peak * world), 4),
+        "node_roofline_basis": "executed kernel work %d M/beacon (prep_sig + prep_msg + MSM, bench/workmodel.json "
+                               "executed_M_per_beacon) at the measured peak" % wm["executed_M_per_beacon"][ex_key],
         "verdicts_ok": ok,
         "streams": S, "warmup_batches": warm_batches,
         "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in prof.items()},
         "stages_ms_single_stream": {k: round(v["total_ms"] / max(1, v["count"]), 3) for k, v in prof1.items()},
+        "single_call": single,
         "sign_seconds": round(t_sign, 2),
     }
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(sch.name, pk, rounds, sigs, args.cpu_sample_seconds, args.cpu_threads)
+        out["cpu_baseline"] = cpu_baseline(sch.name, pk, rounds, sigs, args.cpu_sample_seconds)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -23,6 +23,7 @@
 #include <condition_variable>
 #include <cmath>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -452,10 +453,18 @@ static size_t next_group_size(size_t gsize, size_t ngroups, size_t nfail, size_t
 }
 
 // core pipeline on device-resident inputs
+// Phases of one batch (the node-wide check of dh_batch_begin / dh_batch_finish runs them separately):
+enum verify_mode {
+  VM_FULL = 0,        // prepare, then every level (local level-0 check)
+  VM_BEGIN = 1,       // prepare and the level-0 MSM only: the partial sums are left in outA / outB
+  VM_FINISH = 2,      // after VM_BEGIN: local level-0 check and bisection
+  VM_FINISH_PASS = 3  // after VM_BEGIN, the node-wide check passed: every decoded round is valid
+};
+
 int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                 size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
                 uint8_t* d_verdict, uint8_t* d_rand, uint64_t seed, hipStream_t st, uint64_t* stats,
-                const uint8_t* d_msgs32 = nullptr) {
+                const uint8_t* d_msgs32 = nullptr, int mode = VM_FULL) {
   const bool g2 = sig_on_g2(scheme);
   const int sig_len = g2 ? 96 : 48, key_len = g2 ? 48 : 96;
   if ((int)pk_len != key_len) return fail(DH_EINVAL, "public key must be %d bytes for scheme %d", key_len, scheme);
@@ -466,56 +475,58 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
   const size_t aw = jw * 2 / 3;
 
-  // key
-  HIP_TRY(w->key_raw.ensure(96));
-  HIP_TRY(w->key_aff.ensure(48 * 4));  // key-group affine point (G2: 48 words); fixed size keeps the key cache valid
-  HIP_TRY(w->key_ok.ensure(64));  // [0] key status, [32..63] RLC seed
-  uint8_t key_ok = 0;
-  const bool key_hit = w->cached_key_len == pk_len && w->cached_key_g2 == (g2 ? 0 : 1) && !memcmp(w->cached_key, pk, pk_len);
-  if (key_hit) {
-    key_ok = w->cached_key_ok;
-  } else {
-    w->cached_key_len = 0;
-    HIP_TRY(hipMemcpyAsync(w->key_raw.p, pk, pk_len, hipMemcpyHostToDevice, st));
-    HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(),
-                                  w->key_ok.as<uint8_t>(), st));
-    HIP_TRY(hipMemcpyAsync(&key_ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
-  }
-
-  // per-round prep
-  HIP_TRY(w->status.ensure(n));
-  HIP_TRY(w->sig_aff.ensure(n * aw * 4));
-  HIP_TRY(w->q_pts.ensure(n * jw * 4));
-  HIP_TRY(w->scal.ensure(n * 16));
-  HIP_TRY(w->entries.ensure(n * 4));
   timed_launches T(st);
-  HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>" : "k_prep_sig<fp>", [&] {
-    return dh::launch_prep(g2, d_sigs, sig_stride, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), d_rand, st);
-  }));
-  // hash points: of the beacon digests, or of the given 32-byte messages (VerifyRecovered); a chained record
-  // longer than its slot rejects its round (status)
-  HIP_TRY(w->h2c_tmp.ensure(dh::hash_tmp_bytes(g2, n)));
-  HIP_TRY(T.run(d_msgs32 ? (g2 ? "k_prep_msg32<fp2>" : "k_prep_msg32<fp>") : (g2 ? "k_prep_msg<fp2>" : "k_prep_msg<fp>"), [&] {
-    return dh::launch_hash(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, d_msgs32, n,
-                           scheme == DH_SCHEME_CHAINED && d_prevs && !d_msgs32 ? 1 : 0, dst_id(scheme), w->status.as<uint8_t>(),
-                           w->q_pts.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), st);
-  }));
-  uint32_t seedw[8];
-  int rc = make_seed(seed, seedw);
-  if (rc) return rc;
-  uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
-  HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
-  HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), st));
-  HIP_TRY(hipMemsetAsync(d_verdict, 0, n, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  if (!key_hit) {
-    memcpy(w->cached_key, pk, pk_len);
-    w->cached_key_len = pk_len;
-    w->cached_key_g2 = g2 ? 0 : 1;
-    w->cached_key_ok = key_ok;
+  if (mode <= VM_BEGIN) {
+    // key
+    HIP_TRY(w->key_raw.ensure(96));
+    HIP_TRY(w->key_aff.ensure(48 * 4));  // key-group affine point (G2: 48 words); fixed size keeps the key cache valid
+    HIP_TRY(w->key_ok.ensure(64));  // [0] key status, [32..63] RLC seed
+    uint8_t key_ok = 0;
+    const bool key_hit = w->cached_key_len == pk_len && w->cached_key_g2 == (g2 ? 0 : 1) && !memcmp(w->cached_key, pk, pk_len);
+    if (key_hit) {
+      key_ok = w->cached_key_ok;
+    } else {
+      w->cached_key_len = 0;
+      HIP_TRY(hipMemcpyAsync(w->key_raw.p, pk, pk_len, hipMemcpyHostToDevice, st));
+      HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(),
+                                    w->key_ok.as<uint8_t>(), st));
+      HIP_TRY(hipMemcpyAsync(&key_ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
+    }
+
+    // per-round prep
+    HIP_TRY(w->status.ensure(n));
+    HIP_TRY(w->sig_aff.ensure(n * aw * 4));
+    HIP_TRY(w->q_pts.ensure(n * jw * 4));
+    HIP_TRY(w->scal.ensure(n * 16));
+    HIP_TRY(w->entries.ensure(n * 4));
+    HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>" : "k_prep_sig<fp>", [&] {
+      return dh::launch_prep(g2, d_sigs, sig_stride, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), d_rand, st);
+    }));
+    // hash points: of the beacon digests, or of the given 32-byte messages (VerifyRecovered); a chained record
+    // longer than its slot rejects its round (status)
+    HIP_TRY(w->h2c_tmp.ensure(dh::hash_tmp_bytes(g2, n)));
+    HIP_TRY(T.run(d_msgs32 ? (g2 ? "k_prep_msg32<fp2>" : "k_prep_msg32<fp>") : (g2 ? "k_prep_msg<fp2>" : "k_prep_msg<fp>"), [&] {
+      return dh::launch_hash(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, d_msgs32, n,
+                             scheme == DH_SCHEME_CHAINED && d_prevs && !d_msgs32 ? 1 : 0, dst_id(scheme), w->status.as<uint8_t>(),
+                             w->q_pts.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), st);
+    }));
+    uint32_t seedw[8];
+    int rc = make_seed(seed, seedw);
+    if (rc) return rc;
+    uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
+    HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
+    HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), st));
+    HIP_TRY(hipMemsetAsync(d_verdict, 0, n, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (!key_hit) {
+      memcpy(w->cached_key, pk, pk_len);
+      w->cached_key_len = pk_len;
+      w->cached_key_g2 = g2 ? 0 : 1;
+      w->cached_key_ok = key_ok;
+    }
+    if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
+    HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
   }
-  if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
-  HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
 
   // bisection levels: group sizes n, then next_group_size() per level, then per-round leaves (a failing group is re-checked
   // as smaller groups with the same scalars; only rounds of failing pairs reach a per-round pairing check)
@@ -548,14 +559,24 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
                   w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>(), w->part.as<uint32_t>(),
                   w->meta.as<uint32_t>(), 0};
-    HIP_TRY(T.run(msm_names[std::min(level, 7)], [&] {
-      return dh::launch_msm(g2, g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(), w->sig_aff.as<uint32_t>(),
-                            w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st);
-    }));
-    HIP_TRY(T.run(chk_names[std::min(level, 7)], [&] {
-      return group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups, w->key_aff.as<uint32_t>(),
-                         w->pass.as<uint8_t>(), st);
-    }));
+    if (!(level == 0 && mode >= VM_FINISH)) {  // a resumed batch has its level-0 sums from dh_batch_begin
+      HIP_TRY(T.run(msm_names[std::min(level, 7)], [&] {
+        return dh::launch_msm(g2, g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(), w->sig_aff.as<uint32_t>(),
+                              w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st);
+      }));
+    }
+    if (level == 0 && mode == VM_BEGIN) {
+      HIP_TRY(hipStreamSynchronize(st));
+      return DH_OK;
+    }
+    if (level == 0 && mode == VM_FINISH_PASS) {  // the node-wide check covers this batch's single level-0 group
+      HIP_TRY(hipMemsetAsync(w->pass.p, 1, 1, st));
+    } else {
+      HIP_TRY(T.run(chk_names[std::min(level, 7)], [&] {
+        return group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups, w->key_aff.as<uint32_t>(),
+                           w->pass.as<uint8_t>(), st);
+      }));
+    }
     HIP_TRY(dh::launch_mark_groups(w->entries.as<uint32_t>(), m, gsize, w->pass.as<uint8_t>(), w->status.as<uint8_t>(),
                                    d_verdict, st));
     w->h_pass.resize(ngroups);
@@ -1061,18 +1082,20 @@ struct split_cfg {
   size_t chunk = 262144;
   int workers = 8;
 };
-static const split_cfg& split_config() {
-  static const split_cfg c = [] {
-    split_cfg r;
-    const char* e = getenv("DRANDHIP_SPLIT");
-    if (e && *e) {
-      char* end = nullptr;
-      r.chunk = strtoull(e, &end, 10);
-      if (end && *end == ',') r.workers = std::max(1, atoi(end + 1));
-    }
-    return r;
-  }();
-  return c;
+std::mutex g_split_mu;
+split_cfg g_split = [] {
+  split_cfg r;
+  const char* e = getenv("DRANDHIP_SPLIT");
+  if (e && *e) {
+    char* end = nullptr;
+    r.chunk = strtoull(e, &end, 10);
+    if (end && *end == ',') r.workers = std::max(1, atoi(end + 1));
+  }
+  return r;
+}();
+static split_cfg split_config() {
+  std::lock_guard<std::mutex> lk(g_split_mu);
+  return g_split;
 }
 
 int ensure_device() {
@@ -1085,7 +1108,7 @@ int ensure_device() {
 
 template <class F>
 int run_split(size_t n, F&& fn, uint64_t seed) {
-  const split_cfg& cfg = split_config();
+  const split_cfg cfg = split_config();
   size_t nchunks = 1;
   if (cfg.chunk && cfg.workers > 1 && n >= 2 * cfg.chunk) nchunks = (n + cfg.chunk - 1) / cfg.chunk;
   const size_t per = (n + nchunks - 1) / std::max<size_t>(nchunks, 1);
@@ -1241,6 +1264,130 @@ int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t
     HIP_TRY(hipStreamSynchronize(st));
     return DH_OK;
   }, seed);
+}
+
+// ---- node-wide batch check over several processes (one per GPU)
+struct dh_batch {
+  lease* L = nullptr;
+  int scheme = 0;
+  std::vector<uint8_t> pk;
+  const uint64_t* d_rounds = nullptr;
+  const uint8_t* d_sigs = nullptr;
+  size_t sig_stride = 0;
+  const uint8_t* d_prevs = nullptr;
+  size_t prev_stride = 0;
+  const uint32_t* d_prev_lens = nullptr;
+  size_t n = 0;
+  uint8_t* d_verdict = nullptr;
+  uint8_t* d_rand = nullptr;
+  hipStream_t st = nullptr;
+};
+
+int dh_partial_bytes(int scheme) {
+  if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
+  return (int)(2 * (sig_on_g2(scheme) ? JAC_WORDS_G2 : JAC_WORDS_G1) * 4);
+}
+
+int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
+                   size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
+                   uint8_t* d_verdict_out, uint8_t* d_rand_out, uint64_t seed, void* hip_stream, dh_batch** batch_out,
+                   uint8_t* d_partials_out) {
+  if (!batch_out) return fail(DH_EINVAL, "null batch handle");
+  *batch_out = nullptr;
+  if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
+  if (!pk || !d_partials_out || (n && (!d_rounds || !d_sigs || !d_verdict_out))) return fail(DH_EINVAL, "null argument");
+  std::unique_ptr<dh_batch> b(new dh_batch());
+  b->L = new lease();
+  if (b->L->rc) {
+    int rc = b->L->rc;
+    delete b->L;
+    return rc;
+  }
+  int rc = set_device_and_stream(b->L->w);
+  if (!rc && hip_stream) {  // inputs produced on the caller's stream
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, (hipStream_t)hip_stream) != hipSuccess ||
+        hipStreamWaitEvent(b->L->w->stream, ev, 0) != hipSuccess)
+      rc = fail(DH_EDEVICE, "cannot order the batch after the caller's stream");
+    else
+      (void)hipEventDestroy(ev);
+  }
+  b->scheme = scheme;
+  b->pk.assign(pk, pk + pk_len);
+  b->d_rounds = d_rounds;
+  b->d_sigs = d_sigs;
+  b->sig_stride = sig_stride;
+  b->d_prevs = d_prevs;
+  b->prev_stride = prev_stride;
+  b->d_prev_lens = d_prev_lens;
+  b->n = n;
+  b->d_verdict = d_verdict_out;
+  b->d_rand = d_rand_out;
+  b->st = b->L->w->stream;
+  worker* w = b->L->w;
+  const size_t jw = sig_on_g2(scheme) ? JAC_WORDS_G2 : JAC_WORDS_G1;
+  if (!rc)
+    rc = verify_core(w, scheme, pk, pk_len, d_rounds, d_sigs, sig_stride, d_prevs, prev_stride, d_prev_lens, n, d_verdict_out,
+                     d_rand_out, seed, b->st, nullptr, nullptr, VM_BEGIN);
+  if (!rc && n) {  // (A, B) of this batch into the caller's device buffer
+    if (hipMemcpyAsync(d_partials_out, w->outA.p, jw * 4, hipMemcpyDeviceToDevice, b->st) != hipSuccess ||
+        hipMemcpyAsync(d_partials_out + jw * 4, w->outB.p, jw * 4, hipMemcpyDeviceToDevice, b->st) != hipSuccess ||
+        hipStreamSynchronize(b->st) != hipSuccess)
+      rc = fail(DH_EDEVICE, "copying the partial sums failed");
+  } else if (!rc) {  // an empty batch contributes the identity (Z = 0)
+    if (hipMemset(d_partials_out, 0, 2 * jw * 4) != hipSuccess) rc = fail(DH_EDEVICE, "hipMemset failed");
+  }
+  if (rc) {
+    delete b->L;
+    return rc;
+  }
+  *batch_out = b.release();
+  return DH_OK;
+}
+
+int dh_check_partials(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* d_partials, size_t k, int* pass_out) {
+  if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
+  if (!pk || !d_partials || !pass_out || !k) return fail(DH_EINVAL, "bad node-check arguments");
+  const bool g2 = sig_on_g2(scheme);
+  const size_t key_len = g2 ? 48 : 96, jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
+  if (pk_len != key_len) return fail(DH_EINVAL, "public key must be %zu bytes for scheme %d", key_len, scheme);
+  lease L;
+  if (L.rc) return L.rc;
+  worker* w = L.w;
+  int rc = set_device_and_stream(w);
+  if (rc) return rc;
+  hipStream_t st = w->stream;
+  HIP_TRY(w->key_raw.ensure(96));
+  HIP_TRY(w->key_aff.ensure(48 * 4));
+  HIP_TRY(w->key_ok.ensure(64));
+  HIP_TRY(w->outA.ensure(jw * 4));
+  HIP_TRY(w->outB.ensure(jw * 4));
+  HIP_TRY(w->pass.ensure(16));
+  HIP_TRY(hipMemcpyAsync(w->key_raw.p, pk, pk_len, hipMemcpyHostToDevice, st));
+  HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(), w->key_ok.as<uint8_t>(), st));
+  w->cached_key_len = 0;  // key_aff is rewritten here: the batch path re-decodes its key on this worker
+  HIP_TRY(dh::launch_sum_partials(g2, (const uint32_t*)d_partials, k, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st));
+  HIP_TRY(group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), 1, w->key_aff.as<uint32_t>(), w->pass.as<uint8_t>(), st));
+  uint8_t key_ok = 0, pass = 0;
+  HIP_TRY(hipMemcpyAsync(&key_ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&pass, w->pass.p, 1, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
+  *pass_out = pass == 1 ? 1 : 0;
+  return DH_OK;
+}
+
+int dh_batch_finish(dh_batch* b, int node_pass, uint64_t stats_out[4]) {
+  if (!b) return fail(DH_EINVAL, "null batch handle");
+  int rc = DH_OK;
+  if (node_pass >= 0) {
+    rc = verify_core(b->L->w, b->scheme, b->pk.data(), b->pk.size(), b->d_rounds, b->d_sigs, b->sig_stride, b->d_prevs,
+                     b->prev_stride, b->d_prev_lens, b->n, b->d_verdict, b->d_rand, 0, b->st, stats_out, nullptr,
+                     node_pass ? VM_FINISH_PASS : VM_FINISH);
+  }
+  delete b->L;
+  delete b;
+  return rc;
 }
 
 int dh_verify_beacon(int scheme, const uint8_t* pk, size_t pk_len, uint64_t round, const uint8_t* sig, size_t sig_len,
@@ -1446,6 +1593,14 @@ int dh_public_key(int scheme, const uint8_t* sk32, uint8_t* key_out) {
   HIP_TRY(dh::launch_pubkey(kl == 96, w->key_ok.as<uint32_t>(), w->key_raw.as<uint8_t>(), st));
   HIP_TRY(hipMemcpyAsync(key_out, w->key_raw.p, kl, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  return DH_OK;
+}
+
+int dh_set_split(uint64_t chunk_rounds, int workers) {
+  if (workers < 1) return fail(DH_EINVAL, "workers must be >= 1");
+  std::lock_guard<std::mutex> lk(g_split_mu);
+  g_split.chunk = (size_t)chunk_rounds;
+  g_split.workers = workers;
   return DH_OK;
 }
 

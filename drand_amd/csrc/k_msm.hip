@@ -302,6 +302,24 @@ __global__ __launch_bounds__(64) void k_msm_windows(const uint32_t* __restrict__
 }
 
 
+// node-wide check (dh_check_partials): the level-0 sums of k batches, [A_0 | B_0 | A_1 | B_1 ...], added up:
+// thread 0 sums the A points into outA, thread 1 the B points into outB
+template <class F>
+__global__ __launch_bounds__(64) void k_sum_partials(const uint32_t* __restrict__ parts, size_t k, uint32_t* __restrict__ outA,
+                                                     uint32_t* __restrict__ outB) {
+  const int t = threadIdx.x;
+  if (t > 1) return;
+  jac<F> acc = jac_inf<F>();
+  for (size_t i = 0; i < k; i++) acc = jac_add(acc, ld_jac_aos<F>(parts, 2 * i + t));
+  st_jac_aos<F>(t ? outB : outA, 0, acc);
+}
+
+hipError_t launch_sum_partials(int sig_g2, const uint32_t* parts, size_t k, uint32_t* outA, uint32_t* outB, hipStream_t st) {
+  if (sig_g2) hipLaunchKernelGGL(k_sum_partials<fp2>, dim3(1), dim3(64), 0, st, parts, k, outA, outB);
+  else hipLaunchKernelGGL(k_sum_partials<fp>, dim3(1), dim3(64), 0, st, parts, k, outA, outB);
+  return hipGetLastError();
+}
+
 __global__ void k_mark_groups(const uint32_t* __restrict__ entries, size_t m, size_t gsize, const uint8_t* __restrict__ pass,
                               const uint8_t* __restrict__ status, uint8_t* __restrict__ verdict) {
   size_t e = gtid();

@@ -65,6 +65,8 @@ hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngrou
                              uint32_t* out, hipStream_t st);
 hipError_t launch_group_check(int sig_g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_aff,
                               uint8_t* pass, hipStream_t st);
+// node-wide check: sum the k (A, B) level-0 partial-sum pairs laid out [A_0 | B_0 | A_1 | B_1 ...] (Jacobian AoS)
+hipError_t launch_sum_partials(int sig_g2, const uint32_t* parts, size_t k, uint32_t* outA, uint32_t* outB, hipStream_t st);
 hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,
                               uint8_t* verdict, hipStream_t st);
 hipError_t launch_leaf_check(int sig_g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,

@@ -43,9 +43,16 @@ extern "C" {
 #define DH_SCHEME_G1_LEGACY 2    /* "bls-unchained-on-g1":    sig G1 (48 B), key G2 (96 B), G2 hash DST (legacy) */
 #define DH_SCHEME_G1_RFC9380 3   /* "bls-unchained-g1-rfc9380" (quicknet): sig G1, key G2, G1 hash DST */
 
-/* Select the device (bit i of device_mask = HIP device i; 0 = device 0). Idempotent. */
+/*
+ * Select the device: bit i of device_mask = HIP device i, at most one bit (one process per GPU);
+ * 0 = device 0 or the device already selected. Idempotent; asking for another device after initialisation is
+ * DH_EINVAL until dh_shutdown.
+ */
 int dh_init(uint32_t device_mask);
-/* Release all device resources. Calls after this re-initialise lazily. */
+/*
+ * Release all device resources. Safe while other threads are inside calls: their workers are retired and freed
+ * when those calls return. Calls after this re-initialise lazily.
+ */
 void dh_shutdown(void);
 
 /* crypto.SchemeFromName: scheme id or DH_EINVAL */
@@ -60,21 +67,30 @@ int dh_key_len(int scheme);
  *   rounds[i]    round numbers
  *   sigs         n signatures, record i at sigs + i*sig_stride (sig_stride >= dh_sig_len, multiple of 4)
  *   prevs        chained scheme only (NULL otherwise): previous signature of round i at prevs + i*prev_stride;
- *                length prev_lens[i] (or prev_stride when prev_lens is NULL); lengths must be multiples of
- *                4 and <= 96 (0 = no previous signature, 32 = genesis seed, 96 = stored G2 signature)
+ *                length prev_lens[i] (or prev_stride when prev_lens is NULL), any length <= prev_stride: the
+ *                record is hashed as stored, like crypto/schemes.go:106-114 (0 = none, 32 = genesis seed,
+ *                96 = stored G2 signature; a corrupted 31- or 100-byte record simply fails its round).
+ *                prev_lens[i] > prev_stride is DH_EINVAL here and rejects round i on the device entry point.
  *   verdict_out  n bytes: 1 = VerifyBeacon returns nil, 0 = it returns an error
  *   rand_out     n*32 bytes SHA-256(sig) (RandomnessFromSignature) or NULL
  *   seed         0 = draw the random-linear-combination seed from the OS CSPRNG; otherwise deterministic
+ * One call uses several internal HIP streams for large n: the rounds are cut into chunks (262 144 rounds by
+ * default) verified concurrently by up to 8 workers, each chunk a complete batch check, so one caller gets the
+ * overlap of several batches in flight. DRANDHIP_SPLIT="chunk,workers" changes this ("0": one stream per call).
  * Returns DH_OK or a negative error code (no verdicts are valid on error).
  */
 int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* rounds, const uint8_t* sigs,
                     size_t sig_stride, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens, size_t n,
                     uint8_t* verdict_out, uint8_t* rand_out, uint64_t seed);
 
+/* Set the one-call split of dh_verify_batch / dh_verify_batch_device (chunk_rounds 0 = one stream per call). */
+int dh_set_split(uint64_t chunk_rounds, int workers);
+
 /*
- * Same as dh_verify_batch with every array already resident in device memory (HIP device pointers)
- * and the work enqueued on `hip_stream` (a hipStream_t, NULL = an internal stream). Blocks until done.
- * `stats_out` (nullable, host) receives {levels, groups_failed, leaf_rounds, rounds_rejected}.
+ * Same as dh_verify_batch with every array already resident in device memory (HIP device pointers). The inputs
+ * may still be in production on `hip_stream` (a hipStream_t): the library's streams wait for that stream's work
+ * first; NULL = the inputs are ready. Blocks until done. `stats_out` (nullable, host) receives
+ * {levels, groups_failed, leaf_rounds, rounds_rejected} (levels: the deepest chunk's).
  */
 int dh_verify_batch_device(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                            size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens,
@@ -123,10 +139,33 @@ int dh_recover_batch(int scheme, const uint8_t* commits, int t, int n_nodes, con
  * Batch ThresholdScheme.VerifyPartial(pubPoly, msg, partial) (kyber sign/tbls; called per incoming partial at
  * chain/beacon/node.go:150): same input layout as dh_recover_batch; ok_out[k] (one byte per partial, in
  * input order) = 1 when the k-th partial's signature verifies under PubPoly.Eval(index) for its round's
- * message, 0 otherwise. Indices >= n_nodes have no share in the group and are reported invalid.
+ * message, 0 otherwise.
+ * Deviation from kyber, documented: kyber's VerifyPartial evaluates PubPoly.Eval(i) for ANY index i, so a partial
+ * validly signed with f(i+1) for i >= n_nodes would pass there; here indices >= n_nodes have no share in the group
+ * and are reported invalid (and skipped by dh_recover_batch). drand never hands such a partial to the scheme:
+ * chain/beacon/node.go:138-141 rejects indices outside the group before VerifyPartial and the partial cache.
  */
 int dh_verify_partials_batch(int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
                              const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* ok_out);
+
+/*
+ * Node-wide batch check over the GPUs of one node (one process per GPU). Every rank prepares its
+ * shard of rounds and its level-0 random-linear-combination sums with dh_batch_begin, which writes
+ * dh_partial_bytes(scheme) bytes (A = sum r_i sigma_i, B = sum r_i H(m_i), Jacobian) into d_partials_out (device
+ * memory); the ranks all-gather those bytes (RCCL over xGMI); dh_check_partials adds the k gathered pairs and
+ * runs ONE pairing check e(g, sum A) = e(pk, [h] sum B) for the whole node; dh_batch_finish then either accepts
+ * every decoded round (node_pass = 1) or runs the shard's own level-0 check and bisection (node_pass = 0), so the
+ * verdicts are per-round exact either way. node_pass < 0 abandons the batch. The batch keeps one library worker
+ * between begin and finish; the arguments of dh_batch_begin must stay valid until dh_batch_finish returns.
+ */
+typedef struct dh_batch dh_batch;
+int dh_partial_bytes(int scheme);
+int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
+                   size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
+                   uint8_t* d_verdict_out, uint8_t* d_rand_out, uint64_t seed, void* hip_stream, dh_batch** batch_out,
+                   uint8_t* d_partials_out);
+int dh_check_partials(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* d_partials, size_t k, int* pass_out);
+int dh_batch_finish(dh_batch* batch, int node_pass, uint64_t stats_out[4]);
 
 /*
  * Synthetic-chain utilities (test fixtures and benchmark inputs; not part of the verification path):

@@ -1,8 +1,12 @@
-"""CPU, world_size 2 over gloo: the multi-GPU sharding and the whole-node verdict all-gather used by
-bench.py (drand_amd/dist.py). The verification itself is replaced by a deterministic stand-in verdict so
-this runs without a GPU; the exchange is the same code path as on RCCL."""
+"""CPU, world_size 2 and 3 over gloo: the multi-GPU layer of drand_amd/dist.py that bench.py and the chained replay
+use — strong-scaling shards, the chained halo (host-supplied from the store, and exchanged rank to rank), the
+all-gather of per-rank partial-sum bytes in rank order, and the whole-node verdict bitmaps (ranks of unequal size).
+Verification itself runs on the CPU oracle here (test infrastructure standing in for the device, same verdict
+semantics); a corruption sits on the shard boundary, so the next rank's first round must fail through the halo."""
+import json
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -10,7 +14,12 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from drand_amd.dist import gather_verdicts, pack_bits, shard_range, shard_rounds
+from drand_amd.dist import (exchange_halo, gather_partials, gather_verdicts, pack_bits, shard_beacons, shard_range,
+                            shard_rounds, strong_shard)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+CHAINED = "pedersen-bls-chained"
 
 
 def _free_port():
@@ -21,38 +30,68 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, q):
+def _store_with_boundary_fault(boundary):
+    from drand_amd.sync import TrimmedMemStore
+    c = json.load(open(os.path.join(GOLD, "chains.json")))[CHAINED]
+    st = TrimmedMemStore(True)
+    st.put(0, bytes.fromhex(c["prevs"][0]))
+    for r, sig in zip(c["rounds"], c["sigs"]):
+        st.put(r, bytes.fromhex(sig))
+    st.put(boundary, bytes.fromhex(c["sigs"][boundary - 2]))  # round `boundary` stores round boundary-1's signature
+    return st, bytes.fromhex(c["pk"]), c["rounds"][-1]
+
+
+def _worker(rank, world, port, boundary, q):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ctypes as orc
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    rounds = shard_rounds(rank, world, n)
-    verdict = torch.from_numpy((rounds % 7 != 0).astype(np.uint8))  # stand-in for the device verdicts
+    st, pk, last = _store_with_boundary_fault(boundary)
+    rounds, sigs, prevs, missing = shard_beacons(st, rank, world, 1, last)
+    halo = exchange_halo(sigs[-1] if sigs else b"", rank, world)  # rank r-1's last stored signature
+    halo_ok = rank == 0 or halo == prevs[0] == st.get(rounds[0] - 1).signature
+    verdict = torch.tensor([orc.verify_beacon(CHAINED, pk, r, s, p) for r, s, p in zip(rounds, sigs, prevs)],
+                           dtype=torch.uint8)
     parts = gather_verdicts(pack_bits(verdict), world)
+    allp = gather_partials(torch.full((24,), rank + 1, dtype=torch.uint8), world)
     if rank == 0:
-        bits = np.concatenate([p.numpy() for p in parts])
-        q.put(np.unpackbits(bits).tolist())
+        faulty = []
+        for r_, bits in enumerate(parts):
+            lo, hi = shard_range(r_, world, last)
+            v = np.unpackbits(bits.numpy())[:hi - lo]
+            faulty += [lo + 1 + i for i in np.flatnonzero(v == 0)]
+        q.put({"faulty": faulty, "partials": allp.numpy().tolist()})
+    q.put({"rank": rank, "halo_ok": bool(halo_ok), "missing": missing})
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [64, 1000])
-def test_gather_verdicts_world2(n):
+@pytest.mark.parametrize("world,boundary", [(2, 12), (3, 16)])
+def test_sharded_chained_replay_gloo(world, boundary, oracle):
+    """Round `boundary` (the last round of a shard) stores the previous round's signature: it fails, and the next
+    shard's first round fails too because its previous signature is that record — visible only through the halo.
+    The whole-node faulty set equals the serial oracle replay over the unsharded store."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, boundary, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    msgs = [q.get(timeout=180) for _ in range(world + 1)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    per = (n + 7) // 8 * 8
-    expect = []
-    for r in range(2):
-        rounds = shard_rounds(r, 2, n)
-        expect += (rounds % 7 != 0).astype(int).tolist() + [0] * (per - n)
-    assert got == expect
+    res = next(m for m in msgs if "faulty" in m)
+    assert all(m["halo_ok"] for m in msgs if "rank" in m)
+    assert res["faulty"] == [boundary, boundary + 1]
+    st, pk, last = _store_with_boundary_fault(boundary)
+    serial = [r for r in range(1, last + 1)
+              if not oracle.verify_beacon(CHAINED, pk, r, st.get(r).signature, st.get(r).previous_signature)]
+    assert res["faulty"] == serial
+    lo0, hi0 = shard_range(0, world, last)
+    assert hi0 == boundary or world == 3  # world 2: the fault sits exactly on the shard boundary
+    assert res["partials"] == sum(([r + 1] * 24 for r in range(world)), [])
 
 
 def test_shards_partition_rounds():
@@ -63,6 +102,8 @@ def test_shards_partition_rounds():
         spans = [shard_range(r, 3, total) for r in range(3)]
         assert spans[0][0] == 0 and spans[-1][1] == total
         assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        strong = np.concatenate([strong_shard(r, 3, total) for r in range(3)])
+        assert np.array_equal(strong, np.arange(1, total + 1, dtype=np.uint64))
     with pytest.raises(ValueError):
         shard_rounds(2, 2, 5)
 

@@ -17,8 +17,11 @@ SCHEMES = ["pedersen-bls-chained", "pedersen-bls-unchained", "bls-unchained-on-g
 
 @pytest.fixture(scope="module")
 def dh():
+    import torch
     import drand_amd
     from drand_amd import _lib
+    # torch carries its own HIP runtime: bring it up before the library's runtime has created its streams
+    torch.zeros(1, device="cuda")
     lib = _lib.load()
     assert lib.dh_init(0) == 0, _lib.last_error()
     return drand_amd

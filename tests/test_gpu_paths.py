@@ -33,8 +33,11 @@ CHAINED = "pedersen-bls-chained"
 
 @pytest.fixture(scope="module")
 def dh():
+    import torch
     import drand_amd
     from drand_amd import _lib
+    # torch carries its own HIP runtime: bring it up before the library's runtime has created its streams
+    torch.zeros(1, device="cuda")
     assert _lib.load().dh_init(0) == 0, _lib.last_error()
     return drand_amd
 
@@ -372,3 +375,62 @@ def test_sync_from_stream_device(dh):
     q2.put(END)
     done, stored = sync_from_stream(q2, s, pk, TrimmedMemStore(True), up_to=24, window=8)
     assert not done and stored == list(range(1, 13))
+
+
+# ---------------------------------------------------------------- node-wide check (dh_batch_begin / check / finish)
+def test_node_wide_check_protocol(dh):
+    """The multi-GPU protocol of SURVEY.md §8e on one device: two shards begun as two batches, their level-0 sums
+    combined by dh_check_partials (one pairing check), then finished. All-valid shards pass the node check and are
+    accepted without a local check; with a corrupted round in one shard the node check fails and each shard's own
+    check and bisection give exact verdicts (the clean shard passes its local check)."""
+    import ctypes
+    import torch
+    from drand_amd import _lib
+    from drand_amd.dist import gather_partials  # noqa: F401  (the exchange is a concatenation on one device)
+    lib = _lib.load()
+    s = dh.scheme_from_name("bls-unchained-g1-rfc9380")
+    sk = hashlib.sha256(b"node").digest()
+    n = 12000
+    rounds = np.arange(1, n + 1, dtype=np.uint64)
+    sigs = s.sign_beacons(sk, rounds)
+    pk = s.public_key(sk)
+    dev = torch.device("cuda", 0)
+    pb = lib.dh_partial_bytes(s.id)
+    assert pb == 2 * 36 * 4
+
+    def run(sig_arr):
+        half = [(0, 5000), (5000, n)]
+        d_r = torch.from_numpy(rounds.view(np.int64)).to(dev)
+        d_s = torch.from_numpy(sig_arr).to(dev)
+        d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+        parts = torch.zeros(2 * pb, dtype=torch.uint8, device=dev)
+        handles = []
+        for k, (lo, hi) in enumerate(half):
+            b = ctypes.c_void_p()
+            rc = lib.dh_batch_begin(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr() + 8 * lo),
+                                    ctypes.c_void_p(d_s.data_ptr() + 48 * lo), 48, None, 0, None, hi - lo,
+                                    ctypes.c_void_p(d_v.data_ptr() + lo), None, 0, None, ctypes.byref(b),
+                                    ctypes.c_void_p(parts.data_ptr() + k * pb))
+            assert rc == 0, _lib.last_error()
+            handles.append(b)
+        torch.cuda.synchronize()
+        ok = ctypes.c_int(-1)
+        assert lib.dh_check_partials(s.id, pk, len(pk), ctypes.c_void_p(parts.data_ptr()), 2, ctypes.byref(ok)) == 0
+        stats = []
+        for b in handles:
+            st = (ctypes.c_uint64 * 4)()
+            assert lib.dh_batch_finish(b, ok.value, st) == 0, _lib.last_error()
+            stats.append(list(st))
+        torch.cuda.synchronize()
+        return ok.value, d_v.cpu().numpy(), stats
+
+    ok, v, stats = run(sigs)
+    assert ok == 1 and v.all()
+    bad = sigs.copy()
+    bad[7000] = bad[7001]
+    bad[11999, 0] ^= 0x20
+    ok, v, stats = run(bad)
+    assert ok == 0 and np.flatnonzero(v == 0).tolist() == [7000, 11999]
+    assert stats[0][1] == 0 and stats[1][1] >= 1  # the clean shard passed its own level-0 check
+    ref, _ = s.verify_beacons(pk, rounds, bad, seed=5)
+    assert np.array_equal(ref, v.astype(bool))
