@@ -44,15 +44,23 @@ def sign_chain(scheme, sk, first_round, n, genesis_seed, breaks, rng, progress=N
     ends = np.append(starts[1:], n)
     lens = ends - starts
     sigs = np.zeros((n, scheme.sig_len), dtype=np.uint8)
-    heads = [genesis_seed] + [rng.integers(0, 256, 96, dtype=np.uint8).tobytes() for _ in range(len(starts) - 1)]
+    heads = np.zeros((len(starts), 96), dtype=np.uint8)
+    head_len = np.full(len(starts), 96, dtype=np.uint32)
+    heads[0, :len(genesis_seed)] = np.frombuffer(genesis_seed, np.uint8)
+    head_len[0] = len(genesis_seed)
+    heads[1:] = rng.integers(0, 256, (len(starts) - 1, 96), dtype=np.uint8)
     rounds = np.arange(first_round, first_round + n, dtype=np.uint64)
-    for p in range(int(lens.max())):
+    steps = int(lens.max())
+    for p in range(steps):
         live = np.flatnonzero(lens > p)
         idx = starts[live] + p
-        prevs = [heads[j] if p == 0 else sigs[i - 1].tobytes() for j, i in zip(live, idx)]
-        sigs[idx] = scheme.sign_beacons(sk, rounds[idx], prevs)
-        if progress and p % 256 == 0:
-            progress(p, int(lens.max()))
+        if p == 0:
+            prev, plen = heads[live], head_len[live]
+        else:
+            prev, plen = sigs[idx - 1], np.full(len(idx), 96, dtype=np.uint32)
+        sigs[idx] = scheme.sign_beacons(sk, rounds[idx], np.ascontiguousarray(prev), previous_lengths=plen)
+        if progress and p % 512 == 0:
+            progress(p, steps)
     return sigs
 
 

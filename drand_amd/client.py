@@ -109,3 +109,54 @@ class BatchVerifyingClient:
                 if e is not None:
                     raise e
         return errs
+
+
+def marshal_random_data(rec):
+    """encoding/json of client.RandomData (/root/reference/client/random.go:5-10): fields round, randomness,
+    signature, previous_signature in that order, []byte as standard base64, zero values omitted (omitempty)."""
+    import base64
+    import json
+    out = {}
+    if int(rec.get("round", 0)):
+        out["round"] = int(rec["round"])
+    for key in ("randomness", "signature", "previous_signature"):
+        v = bytes(rec.get(key) or b"")
+        if v:
+            out[key] = base64.b64encode(v).decode()
+    return json.dumps(out, separators=(",", ":")).encode()
+
+
+def relay_s3_sync(client, get_record, upload, begin, end, window=4096, log=None):
+    """relay-s3 `sync` (/root/reference/cmd/relay-s3/main.go:182-195) with the per-round verify batched: rounds
+    begin..end are fetched window by window (get_record(round) -> RandomData dict or raises, the verifying client's
+    Get), every fetched window is verified in ONE batch (BatchVerifyingClient.verify_many: the same verdicts and
+    randomness as verifyingClient.verify per round), and each verified round is uploaded as upload(key, body) with
+    key "public/<round>" and body the JSON of client.RandomData. As in the reference, a failed fetch, verification or
+    upload is logged and skipped (the loop goes on). Returns the uploaded rounds in order."""
+    uploaded = []
+
+    def note(*a):
+        if log is not None:
+            log(*a)
+
+    for lo in range(int(begin), int(end) + 1, window):
+        recs = []
+        for rnd in range(lo, min(int(end), lo + window - 1) + 1):
+            try:
+                recs.append(dict(get_record(rnd)))
+            except Exception as e:  # noqa: BLE001 - the reference logs and continues
+                note("failed to get randomness", rnd, e)
+        if not recs:
+            continue
+        errs = client.verify_many(recs)
+        for rec, err in zip(recs, errs):
+            if err is not None:
+                note("failed to get randomness", rec.get("round"), err)
+                continue
+            try:
+                upload("public/%d" % int(rec["round"]), marshal_random_data(rec))
+            except Exception as e:  # noqa: BLE001
+                note("failed to upload randomness", e)
+                continue
+            uploaded.append(int(rec["round"]))
+    return uploaded

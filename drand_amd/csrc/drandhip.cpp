@@ -98,7 +98,7 @@ struct worker {
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
-      r_sigbytes, r_status2, r_aff2, r_entries2;
+      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den;
   std::vector<uint8_t> h_pass;
   std::vector<uint8_t> h_verdict;
   // decoded group key cache: the same key is used for every batch of a chain
@@ -113,7 +113,7 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2};
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
@@ -838,55 +838,38 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     return dh::launch_hash(g2, nullptr, nullptr, 0, nullptr, w->r_msgs.as<uint8_t>(), n_rounds, 0, dst_id(scheme), nullptr,
                            w->r_q.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), st);
   }));
-  // 6. per-partial round, share index (host parse), signer-sorted entry lists
-  std::vector<uint32_t> round_of(np), share(np);
-  for (size_t j = 0; j < n_rounds; j++)
-    for (uint32_t e = part_off[j]; e < part_off[j + 1]; e++) round_of[e - base] = (uint32_t)j;
-  for (size_t e = 0; e < np; e++) {
-    const uint8_t* r = partials + (size_t)(base + e) * (2 + sl);
-    share[e] = ((uint32_t)r[0] << 8) | r[1];
-  }
-  std::vector<uint32_t> cnt(n_nodes + 1, 0);
-  for (size_t e = 0; e < np; e++)
-    if (share[e] < (uint32_t)n_nodes) cnt[share[e] + 1]++;
-  for (int i = 0; i < n_nodes; i++) cnt[i + 1] += cnt[i];
-  const size_t mB = cnt[n_nodes];
-  std::vector<uint32_t> e_pidx(mB), e_sidx(mB), e_grp(mB), cur(cnt.begin(), cnt.end() - 1);
-  for (size_t e = 0; e < np; e++) {
-    if (share[e] >= (uint32_t)n_nodes) continue;
-    uint32_t pos = cur[share[e]]++;
-    e_pidx[pos] = round_of[e];
-    e_sidx[pos] = (uint32_t)e;
-    e_grp[pos] = share[e];
-  }
+  // 6. per-partial round and the group-membership rule, on the device (offsets relative to the first partial)
+  std::vector<uint32_t> off_rel(n_rounds + 1);
+  for (size_t j = 0; j <= n_rounds; j++) off_rel[j] = part_off[j] - base;
+  HIP_TRY(w->r_off.ensure((n_rounds + 1) * 4));
   HIP_TRY(w->r_round_of.ensure(np * 4 + 4));
-  HIP_TRY(w->r_e_pidx.ensure(mB * 4 + 4));
-  HIP_TRY(w->r_e_sidx.ensure(mB * 4 + 4));
-  HIP_TRY(w->r_e_grp.ensure(mB * 4 + 4));
-  HIP_TRY(hipMemcpyAsync(w->r_round_of.p, round_of.data(), np * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(w->r_e_pidx.p, e_pidx.data(), mB * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(w->r_e_sidx.p, e_sidx.data(), mB * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(w->r_e_grp.p, e_grp.data(), mB * 4, hipMemcpyHostToDevice, st));
-  // 7. RLC scalars per partial
+  HIP_TRY(hipMemcpyAsync(w->r_off.p, off_rel.data(), (n_rounds + 1) * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(dh::launch_partial_meta(w->r_off.as<uint32_t>(), n_rounds, w->r_pidx.as<uint32_t>(), n_nodes,
+                                  w->r_round_of.as<uint32_t>(), w->r_pstatus.as<uint8_t>(), st));
+  // 7. RLC scalars per partial (0 for partials that failed decoding or lie outside the group)
   uint32_t seedw[8];
   int rc = make_seed(0, seedw);
   if (rc) return rc;
   HIP_TRY(w->key_ok.ensure(64));
   uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
   HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
-  HIP_TRY(w->r_scal.ensure(np * 16 + 16));
+  HIP_TRY(w->r_scal.ensure(std::max(np, n_rounds) * 16 + 16));
   HIP_TRY(dh::launch_scalars(d_seed, np, w->r_pstatus.as<uint8_t>(), w->r_scal.as<uint4>(), st));
   HIP_TRY(hipStreamSynchronize(st));
   for (int c = 0; c < t; c++)
     if (cst[c] != 1) return fail(DH_EKEY, "public polynomial commitment %d does not decode to a subgroup point", c);
-  // 8./9. MSMs: A = sum r sigma (one group), B_i = sum r Q_round per signer i
+  // 8./9. MSMs: A = sum r sigma (one group), B_i = sum r Q_round per signer i: entry e -> point round_of[e], scalar e,
+  // group min(share, n-1) (the sort keys by (group, window, digit), so the entries need no order; a zero scalar
+  // contributes nothing)
   HIP_TRY(w->r_ok.ensure(np + 4));
   bool batch_ok = false;
   {
     HIP_TRY(w->entries.ensure(np * 4 + 4));
     HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), np, st));
+    HIP_TRY(w->r_e_grp.ensure(np * 4 + 4));
+    HIP_TRY(dh::launch_clamp_group(w->r_pidx.as<uint32_t>(), np, (uint32_t)n_nodes - 1, w->r_e_grp.as<uint32_t>(), st));
     const dh::msm_geom gA = geom_for(std::max<size_t>(np, 1));
-    size_t avg = std::max<size_t>(1, mB / std::max(1, n_nodes));
+    size_t avg = std::max<size_t>(1, np / std::max(1, n_nodes));
     dh::msm_geom gB = geom_for(avg);
     while (gB.c > 3 && (size_t)n_nodes * gB.nwin * gB.nbuck > ((size_t)1 << 24)) gB = geom_for(((size_t)1 << (gB.c + 1)));
     const size_t nkA = (size_t)gA.nwin * gA.nbuck, nkB = (size_t)n_nodes * gB.nwin * gB.nbuck;
@@ -894,13 +877,13 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(w->cnt.ensure(nk * 4));
     HIP_TRY(w->off.ensure((nk + 1) * 4));
     HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
-    HIP_TRY(w->list.ensure(std::max(np * gA.nwin, mB * gB.nwin) * 4 + 4));
+    HIP_TRY(w->list.ensure(std::max(np * gA.nwin, np * gB.nwin) * 4 + 4));
     HIP_TRY(w->buckets.ensure(nk * jw * 4));
     HIP_TRY(w->segs.ensure(std::max((size_t)gA.nwin * gA.nseg, (size_t)n_nodes * gB.nwin * gB.nseg) * jw * 4));
     HIP_TRY(w->outA.ensure(jw * 4));
     HIP_TRY(w->outB.ensure((size_t)n_nodes * jw * 4));
     // chunk length depends on the list length: size for each of the two MSMs, not for the longer list
-    const size_t entA = np * gA.nwin, entB = mB * gB.nwin;
+    const size_t entA = np * gA.nwin, entB = np * gB.nwin;
     HIP_TRY(w->part.ensure(std::max(dh::msm_part_bytes(entA, jw, 1), dh::msm_part_bytes(entB, jw, 1))));
     HIP_TRY(w->meta.ensure(std::max(dh::msm_meta_bytes(entA), dh::msm_meta_bytes(entB))));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
@@ -912,8 +895,8 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
       return dh::launch_msm_points(g2, 1, gA, 1, w->r_paff.as<uint32_t>(), ws, w->outA.as<uint32_t>(), st);
     }));
     HIP_TRY(T.run("recover_msm_hash_by_signer", [&] {
-      hipError_t e = dh::launch_msm_sort(gB, w->r_e_pidx.as<uint32_t>(), w->r_e_sidx.as<uint32_t>(), w->r_e_grp.as<uint32_t>(),
-                                         mB, n_nodes, w->r_scal.as<uint4>(), ws, st);
+      hipError_t e = dh::launch_msm_sort(gB, w->r_round_of.as<uint32_t>(), w->entries.as<uint32_t>(), w->r_e_grp.as<uint32_t>(),
+                                         np, n_nodes, w->r_scal.as<uint4>(), ws, st);
       if (e != hipSuccess) return e;
       return dh::launch_msm_points(g2, 0, gB, n_nodes, w->r_q.as<uint32_t>(), ws, w->outB.as<uint32_t>(), st);
     }));
@@ -941,75 +924,41 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(hipStreamSynchronize(st));
     batch_ok = pass == 1;
   }
-  // 11. per-partial validity
-  std::vector<uint8_t> ok(np);
+  // 11. per-partial validity, on the device
   if (batch_ok) {
-    HIP_TRY(hipMemcpyAsync(ok.data(), w->r_pstatus.p, np, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    for (size_t e = 0; e < np; e++) ok[e] = (ok[e] == 1 && share[e] < (uint32_t)n_nodes) ? 1 : 0;
+    HIP_TRY(dh::launch_ok_from_status(w->r_pstatus.as<uint8_t>(), np, w->r_ok.as<uint8_t>(), st));
   } else {
     HIP_TRY(T.run("k_partial_leaf", [&] {
       return dh::launch_partial_leaf(g2, w->entries.as<uint32_t>(), np, w->r_paff.as<uint32_t>(), w->r_pstatus.as<uint8_t>(),
                                      w->r_pidx.as<uint32_t>(), w->r_round_of.as<uint32_t>(), w->r_q.as<uint32_t>(),
                                      w->r_shares.as<uint32_t>(), n_nodes, w->r_ok.as<uint8_t>(), st);
     }));
-    HIP_TRY(hipMemcpyAsync(ok.data(), w->r_ok.p, np, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
   }
   if (partial_ok_out) {  // dh_verify_partials_batch: per-partial VerifyPartial verdicts only
-    memcpy(partial_ok_out, ok.data(), np);
+    HIP_TRY(hipMemcpyAsync(partial_ok_out, w->r_ok.p, np, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     return DH_OK;
   }
-  // 12. selection (first t valid in the given order; sorted by index; duplicates dropped) + Lagrange sets
-  std::vector<uint32_t> sel(n_rounds * (size_t)t, 0), lamset(n_rounds, 0);
-  std::vector<uint8_t> rok(n_rounds, 0);
-  std::vector<std::vector<uint32_t>> sets;
-  std::vector<uint32_t> lam;
-  std::map<std::vector<uint32_t>, uint32_t> set_id;
-  for (size_t j = 0; j < n_rounds; j++) {
-    std::vector<std::pair<uint32_t, uint32_t>> kept;  // (share index, partial id)
-    for (uint32_t e = part_off[j] - base; e < part_off[j + 1] - base && kept.size() < (size_t)t; e++)
-      if (ok[e]) kept.emplace_back(share[e], e);
-    if (kept.size() < (size_t)t) continue;
-    std::stable_sort(kept.begin(), kept.end(), [](auto& a, auto& b) { return a.first < b.first; });
-    std::vector<uint32_t> idx;
-    std::vector<uint32_t> pid;
-    for (auto& k : kept) {
-      if (!idx.empty() && idx.back() == k.first) continue;
-      idx.push_back(k.first);
-      pid.push_back(k.second);
-    }
-    if (idx.size() < (size_t)t) continue;
-    auto it = set_id.find(idx);
-    uint32_t sid;
-    if (it == set_id.end()) {
-      sid = (uint32_t)sets.size();
-      set_id.emplace(idx, sid);
-      sets.push_back(idx);
-      lam.resize(lam.size() + (size_t)t * 16);
-      lagrange_at_zero(idx, lam.data() + (size_t)sid * t * 16);
-    } else {
-      sid = it->second;
-    }
-    for (int k = 0; k < t; k++) sel[j * t + k] = pid[k];
-    lamset[j] = sid;
-    rok[j] = 1;
-  }
-  if (sets.empty()) lam.assign((size_t)t * 16, 0);
-  // 13. interpolation on the device
-  HIP_TRY(w->r_sel.ensure(sel.size() * 4));
-  HIP_TRY(w->r_lam.ensure(lam.size() * 4));
-  HIP_TRY(w->r_lamset.ensure(n_rounds * 4));
+  // 12. selection (first t valid in the given order; sorted by index; duplicates dropped) + Lagrange coefficients,
+  // one lane per round
+  HIP_TRY(w->r_sel.ensure(n_rounds * (size_t)t * 4));
+  HIP_TRY(w->r_key.ensure(n_rounds * (size_t)t * 4));
+  HIP_TRY(w->r_den.ensure(n_rounds * (size_t)t * 32));
+  HIP_TRY(w->r_lam.ensure(n_rounds * (size_t)t * 64));
   HIP_TRY(w->r_rok.ensure(n_rounds));
   HIP_TRY(w->r_sig.ensure(n_rounds * jw * 4));
-  HIP_TRY(hipMemcpyAsync(w->r_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(w->r_lam.p, lam.data(), lam.size() * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(w->r_lamset.p, lamset.data(), n_rounds * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipMemcpyAsync(w->r_rok.p, rok.data(), n_rounds, hipMemcpyHostToDevice, st));
-  HIP_TRY(T.run("k_lagrange", [&] {
-    return dh::launch_lagrange(g2, w->r_sel.as<uint32_t>(), w->r_lam.as<uint32_t>(), w->r_lamset.as<uint32_t>(),
-                               w->r_rok.as<uint8_t>(), t, n_rounds, w->r_paff.as<uint32_t>(), w->r_sig.as<uint32_t>(), st);
+  HIP_TRY(T.run("k_select_lagrange", [&] {
+    return dh::launch_select_lagrange(w->r_off.as<uint32_t>(), w->r_ok.as<uint8_t>(), w->r_pidx.as<uint32_t>(), t, n_rounds,
+                                      w->r_sel.as<uint32_t>(), w->r_key.as<uint32_t>(), w->r_den.as<uint32_t>(),
+                                      w->r_lam.as<uint32_t>(), w->r_rok.as<uint8_t>(), st);
   }));
+  // 13. interpolation on the device
+  HIP_TRY(T.run("k_lagrange", [&] {
+    return dh::launch_lagrange(g2, w->r_sel.as<uint32_t>(), w->r_lam.as<uint32_t>(), nullptr, w->r_rok.as<uint8_t>(), t,
+                               n_rounds, w->r_paff.as<uint32_t>(), w->r_sig.as<uint32_t>(), st);
+  }));
+  std::vector<uint8_t> rok(n_rounds, 0);
+  HIP_TRY(hipMemcpyAsync(rok.data(), w->r_rok.p, n_rounds, hipMemcpyDeviceToHost, st));
   // 14./15. compress, then VerifyRecovered (chainstore.go:207) as one batch against the group key (commit 0)
   HIP_TRY(w->r_sigbytes.ensure(n_rounds * sl));
   HIP_TRY(dh::launch_compress(g2, w->r_sig.as<uint32_t>(), n_rounds, w->r_sigbytes.as<uint8_t>(), st));

@@ -8,9 +8,12 @@
 //   k_pair_miller       one lane per pair of the multi-pairing prod_i e(pk_i, B_i) e(-g, A) -> Miller value
 //   k_pair_product      one lane: product of the Miller values, final exponentiation, == 1
 //   k_partial_leaf      per-partial VerifyPartial (only when the batch check fails)
-//   k_lagrange          per round: sum_k lambda_k sigma_k (Straus, shared doublings), lambda from the host
+//   k_partial_meta      per round: the round of each partial; indices outside the group are rejected
+//   k_select_lagrange   per round: first t valid partials, index order, duplicates dropped, Lagrange at 0 (F_r)
+//   k_lagrange          per round: sum_k lambda_k sigma_k (Straus, shared doublings)
 //   k_compress          recovered signatures -> compressed bytes
 #include "kcommon.hpp"
+#include "fr.hpp"
 
 namespace dh {
 
@@ -87,6 +90,115 @@ __global__ void k_pair_product(const uint32_t* __restrict__ f_in, const uint8_t*
   *pass = fp12_is_one(final_exp(acc)) ? 1 : 0;
 }
 
+// one lane per round j: round_of[e] = j for its partials e in [off[j], off[j+1]) (offsets relative to the first
+// partial); a share index outside the group has no public share (include/drandhip.h): status -> DEC_BAD, so its RLC
+// scalar is 0 and the batch check ignores it
+__global__ __launch_bounds__(256) void k_partial_meta(const uint32_t* __restrict__ off, size_t n_rounds,
+                                                      const uint32_t* __restrict__ share_idx, int n_nodes,
+                                                      uint32_t* __restrict__ round_of, uint8_t* __restrict__ status) {
+  size_t j = gtid();
+  if (j >= n_rounds) return;
+  for (uint32_t e = off[j]; e < off[j + 1]; e++) {
+    round_of[e] = (uint32_t)j;
+    if (share_idx[e] >= (uint32_t)n_nodes) status[e] = DEC_BAD;
+  }
+}
+
+// MSM group of partial e for the per-signer sums: its share index (those outside the group carry a zero scalar)
+__global__ __launch_bounds__(256) void k_clamp_group(const uint32_t* __restrict__ share_idx, size_t np, uint32_t hi,
+                                                     uint32_t* __restrict__ grp) {
+  size_t e = gtid();
+  if (e < np) grp[e] = min(share_idx[e], hi);
+}
+
+// after the batch check: ok[e] = 1 iff partial e decoded (subgroup point, index inside the group)
+__global__ __launch_bounds__(256) void k_ok_from_status(const uint8_t* __restrict__ status, size_t np, uint8_t* __restrict__ ok) {
+  size_t e = gtid();
+  if (e < np) ok[e] = status[e] == DEC_OK ? 1 : 0;
+}
+
+// Recover's selection and Lagrange basis per round, one lane per round (kyber v1.1.18 tbls.Recover +
+// share.RecoverCommit / xyCommit, restated in oracle/bls_oracle.c or_recover): the first t valid partials in arrival
+// order (Recover stops at t), sorted by share index (stable), duplicate indices dropped; fewer than t distinct ->
+// not recovered. Then lambda_k = prod_{m != k} x_m / (x_m - x_k) over x = index + 1 in F_r (one batch inversion),
+// written as NAF digit masks for k_lagrange. sel/key: t words per round; den: 8 t words per round (scratch);
+// lam: 16 t words per round.
+__global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restrict__ off, const uint8_t* __restrict__ ok,
+                                                        const uint32_t* __restrict__ share_idx, int t, size_t n_rounds,
+                                                        uint32_t* __restrict__ sel, uint32_t* __restrict__ key,
+                                                        uint32_t* __restrict__ den, uint32_t* __restrict__ lam,
+                                                        uint8_t* __restrict__ rok) {
+  const size_t j = gtid();
+  if (j >= n_rounds) return;
+  uint32_t* S = sel + j * (size_t)t;
+  uint32_t* K = key + j * (size_t)t;
+  int kept = 0;
+  for (uint32_t e = off[j]; e < off[j + 1] && kept < t; e++) {
+    if (!ok[e]) continue;
+    const uint32_t ki = share_idx[e];
+    int pos = kept;
+    while (pos > 0 && K[pos - 1] > ki) {
+      K[pos] = K[pos - 1];
+      S[pos] = S[pos - 1];
+      pos--;
+    }
+    K[pos] = ki;
+    S[pos] = e;
+    kept++;
+  }
+  int nd = 0;
+  for (int a = 0; a < kept; a++) {
+    if (nd && K[nd - 1] == K[a]) continue;
+    K[nd] = K[a];
+    S[nd] = S[a];
+    nd++;
+  }
+  if (nd < t) {
+    rok[j] = 0;
+    return;
+  }
+  rok[j] = 1;
+  uint32_t* D = den + j * (size_t)t * 8;
+  uint32_t* L = lam + j * (size_t)t * 16;
+  // pass 1: numerators (into lam's second half), denominators (scratch), prefix products (into lam's first half)
+  fr pre = fr_one();
+  for (int k = 0; k < t; k++) {
+    const fr xk = fr_from_u32(K[k] + 1);
+    fr num = fr_one(), dk = fr_one();
+    for (int m = 0; m < t; m++) {
+      if (m == k) continue;
+      const fr xm = fr_from_u32(K[m] + 1);
+      num = fr_mul(num, xm);
+      dk = fr_mul(dk, fr_sub(xm, xk));
+    }
+    for (int w = 0; w < 8; w++) {
+      L[16 * k + w] = pre.v[w];
+      L[16 * k + 8 + w] = num.v[w];
+      D[8 * k + w] = dk.v[w];
+    }
+    pre = fr_mul(pre, dk);
+  }
+  // pass 2: one inversion of the product, then lambda_k from the back
+  fr inv = fr_inv(pre);
+  for (int k = t - 1; k >= 0; k--) {
+    fr pk, nk, dk;
+    for (int w = 0; w < 8; w++) {
+      pk.v[w] = L[16 * k + w];
+      nk.v[w] = L[16 * k + 8 + w];
+      dk.v[w] = D[8 * k + w];
+    }
+    const fr dinv = fr_mul(inv, pk);
+    inv = fr_mul(inv, dk);
+    uint32_t words[8], pos[8], neg[8];
+    fr_to_words(fr_mul(nk, dinv), words);
+    fr_naf_masks(words, pos, neg);
+    for (int w = 0; w < 8; w++) {
+      L[16 * k + w] = pos[w];
+      L[16 * k + 8 + w] = neg[w];
+    }
+  }
+}
+
 // VerifyPartial for each listed partial e: pubshare = shares[idx[e]], hash point q[round_of[e]]
 template <class F>
 __global__ __launch_bounds__(64) void k_partial_leaf(const uint32_t* __restrict__ list, size_t m,
@@ -122,7 +234,7 @@ __global__ __launch_bounds__(64) void k_partial_leaf(const uint32_t* __restrict_
 }
 
 // sigma_j = sum_k lambda_{j,k} sigma_{sel[j,k]}: Straus over t points with shared doublings.
-// lam: nsets x t x 8 words (little-endian 256-bit scalars mod r); lam_set[j] selects the row set.
+// lam: per term the NAF masks of lambda (16 words); row set lam_set[j], or the round's own rows when lam_set is null.
 // LG_LANES lanes per round, each running Straus (shared doublings) over every LG_LANES-th term of the
 // interpolation sum sum_k lambda_k sigma_k; the partial sums meet in LDS and the first lane of the round adds
 // them. One lane per round left most of the chip idle at 10^4-10^5 rounds and ran 33 terms x 127 additions
@@ -141,7 +253,7 @@ __global__ __launch_bounds__(64) void k_lagrange(const uint32_t* __restrict__ se
   const int q = (int)(tid % LG_LANES);
   jac<F> acc = jac_inf<F>();
   if (j < n_rounds && ok[j]) {
-    const uint32_t* L = lam + (size_t)lam_set[j] * t * 16;  // per term: NAF positive mask, negative mask
+    const uint32_t* L = lam + (lam_set ? (size_t)lam_set[j] : j) * t * 16;  // per term: NAF positive mask, negative mask
     const uint32_t* S = sel + j * (size_t)t;
     const int nt = (t - q + LG_LANES - 1) / LG_LANES;  // terms of this lane: k = q + LG_LANES i
     // digit masks of the current 32-bit chunk and the point indices live in LDS (dynamic indices, no scratch)
@@ -248,6 +360,34 @@ hipError_t launch_partial_leaf(int sig_g2, const uint32_t* list, size_t m, const
   else
     hipLaunchKernelGGL(k_partial_leaf<fp>, dim3(nblk(m, 64)), dim3(64), 0, st, list, m, sig_aff, status, share_idx, round_of,
                        q_pts, shares, n_nodes, ok_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_partial_meta(const uint32_t* off, size_t n_rounds, const uint32_t* share_idx, int n_nodes, uint32_t* round_of,
+                               uint8_t* status, hipStream_t st) {
+  if (!n_rounds) return hipSuccess;
+  hipLaunchKernelGGL(k_partial_meta, dim3(nblk(n_rounds, 256)), dim3(256), 0, st, off, n_rounds, share_idx, n_nodes, round_of,
+                     status);
+  return hipGetLastError();
+}
+
+hipError_t launch_clamp_group(const uint32_t* share_idx, size_t np, uint32_t hi, uint32_t* grp, hipStream_t st) {
+  if (!np) return hipSuccess;
+  hipLaunchKernelGGL(k_clamp_group, dim3(nblk(np, 256)), dim3(256), 0, st, share_idx, np, hi, grp);
+  return hipGetLastError();
+}
+
+hipError_t launch_ok_from_status(const uint8_t* status, size_t np, uint8_t* ok, hipStream_t st) {
+  if (!np) return hipSuccess;
+  hipLaunchKernelGGL(k_ok_from_status, dim3(nblk(np, 256)), dim3(256), 0, st, status, np, ok);
+  return hipGetLastError();
+}
+
+hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const uint32_t* share_idx, int t, size_t n_rounds,
+                                  uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint8_t* rok, hipStream_t st) {
+  if (!n_rounds) return hipSuccess;
+  hipLaunchKernelGGL(k_select_lagrange, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, off, ok, share_idx, t, n_rounds, sel, key,
+                     den, lam, rok);
   return hipGetLastError();
 }
 

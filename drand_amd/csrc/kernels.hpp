@@ -96,6 +96,14 @@ hipError_t launch_pair_check(const uint32_t* P, const uint32_t* Q, size_t npairs
 hipError_t launch_partial_leaf(int sig_g2, const uint32_t* list, size_t m, const uint32_t* sig_aff, const uint8_t* status,
                                const uint32_t* share_idx, const uint32_t* round_of, const uint32_t* q_pts,
                                const uint32_t* shares, int n_nodes, uint8_t* ok_out, hipStream_t st);
+// per round: round_of for its partials, indices >= n_nodes rejected (status); ok from status after a passed batch
+hipError_t launch_partial_meta(const uint32_t* off, size_t n_rounds, const uint32_t* share_idx, int n_nodes, uint32_t* round_of,
+                               uint8_t* status, hipStream_t st);
+hipError_t launch_clamp_group(const uint32_t* share_idx, size_t np, uint32_t hi, uint32_t* grp, hipStream_t st);
+hipError_t launch_ok_from_status(const uint8_t* status, size_t np, uint8_t* ok, hipStream_t st);
+// per round: Recover's selection + Lagrange coefficients (sel/key: t words, den: 8t words, lam: 16t words per round)
+hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const uint32_t* share_idx, int t, size_t n_rounds,
+                                  uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint8_t* rok, hipStream_t st);
 hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
                            int t, size_t n_rounds, const uint32_t* sig_aff, uint32_t* out, hipStream_t st);
 hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, hipStream_t st);

@@ -212,6 +212,24 @@ class Scheme:
                                             _ptr(sigs), _ptr(ok)))
         return sigs, ok.astype(bool)
 
+    def recover_batch_packed(self, commits, t, n, msgs, raw, offsets):
+        """recover_batch over caller-packed columns: msgs (n_rounds, 32) uint8, raw (n_partials, 2 + sig_len) uint8
+        records (2-byte BE index || signature), offsets (n_rounds + 1,) uint32 into raw."""
+        commits = b"".join(bytes(c) for c in commits)
+        if len(commits) != t * self.key_len:
+            raise SchemeError("need t commitments of %d bytes" % self.key_len)
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        raw = np.ascontiguousarray(raw, dtype=np.uint8)
+        off = np.ascontiguousarray(offsets, dtype=np.uint32)
+        n_rounds = len(msgs)
+        if msgs.shape != (n_rounds, 32) or off.shape != (n_rounds + 1,) or raw.ndim != 2 or raw.shape[1] != 2 + self.sig_len:
+            raise SchemeError("bad packed Recover columns")
+        sigs = np.zeros((n_rounds, self.sig_len), dtype=np.uint8)
+        ok = np.zeros(n_rounds, dtype=np.uint8)
+        _check(_lib.load().dh_recover_batch(self.id, commits, int(t), int(n), _ptr(msgs), _ptr(raw), _ptr(off), n_rounds,
+                                            _ptr(sigs), _ptr(ok)))
+        return sigs, ok.astype(bool)
+
     def recover(self, commits, msg, partials, t, n):
         """ThresholdScheme.Recover(pubPoly, msg, sigs, t, n): the recovered signature, or SchemeError."""
         sigs, ok = self.recover_batch(commits, t, n, [msg], [partials])
@@ -226,13 +244,15 @@ class Scheme:
         return out
 
     # ---- synthetic-chain utilities (tests / bench): device signer
-    def sign_beacons(self, secret32, rounds, previous_signatures=None):
+    def sign_beacons(self, secret32, rounds, previous_signatures=None, previous_lengths=None):
         rounds = np.ascontiguousarray(rounds, dtype=np.uint64)
         n = len(rounds)
         prev = plen = None
         pstride = 0
         if self.chained and previous_signatures is not None:
             prev, plen, pstride = _pack_prevs(previous_signatures, n)
+            if previous_lengths is not None:
+                plen = np.ascontiguousarray(previous_lengths, dtype=np.uint32)
         out = np.zeros((n, self.sig_len), dtype=np.uint8)
         _check(_lib.load().dh_sign_batch(self.id, bytes(secret32), _ptr(rounds), _ptr(prev), n if prev is None else n,
                                          _ptr(plen) if plen is not None else None, pstride, _ptr(out)))

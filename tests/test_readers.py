@@ -182,3 +182,49 @@ def test_stream_sync_windows(oracle):
     wrong_id[5]["beacon_id"] = "other"
     done, stored = sync_from_stream(wrong_id, s, pk, TrimmedMemStore(False), up_to=24, window=4)
     assert not done and stored == list(range(1, 6))
+
+
+def _serial_relay_s3(scheme, pk, get, begin, end):
+    """cmd/relay-s3/main.go:182-195 serially: Get (fetch + verifyingClient.verify), upload, log-and-continue."""
+    out = []
+    for rnd in range(begin, end + 1):
+        try:
+            r = get(rnd)
+        except KeyError:
+            continue
+        prev = r["previous_signature"] if scheme.chained else b""
+        if len(r["signature"]) != scheme.sig_len or not scheme.verify_beacons(pk, [rnd], [r["signature"]], [prev])[0][0]:
+            continue
+        out.append(rnd)
+    return out
+
+
+def test_relay_s3_range_sync(oracle):
+    """relay-s3 sync batched per window: the same uploaded rounds as the serial loop (missing rounds and a round
+    whose signature belongs to another round are skipped), bodies = encoding/json of client.RandomData
+    (base64 []byte, omitempty) with randomness = SHA-256(signature)."""
+    import base64
+    import hashlib
+    from drand_amd.client import marshal_random_data, relay_s3_sync
+    c = json.load(open(os.path.join(GOLD, "chains.json")))["pedersen-bls-chained"]
+    s = OracleScheme(oracle, "pedersen-bls-chained")
+    info = Info(bytes.fromhex(c["pk"]), 30, s.name, 0, bytes.fromhex(c["prevs"][0]))
+    recs = {r: {"round": r, "signature": bytes.fromhex(x), "previous_signature": bytes.fromhex(p)}
+            for r, x, p in zip(c["rounds"], c["sigs"], c["prevs"])}
+    del recs[6]
+    recs[9] = dict(recs[9], signature=recs[10]["signature"])
+
+    def get(r):
+        return dict(recs[r])
+
+    bucket = {}
+    cl = BatchVerifyingClient(info, s)
+    up = relay_s3_sync(cl, get, lambda k, b: bucket.__setitem__(k, b), 1, 24, window=5)
+    assert len(s.calls) == 5  # one verification batch per window
+    assert up == _serial_relay_s3(s, info.public_key, get, 1, 24)
+    assert 6 not in up and 9 not in up and len(up) == 22
+    body = json.loads(bucket["public/3"])
+    assert list(body) == ["round", "randomness", "signature", "previous_signature"]
+    assert body["round"] == 3 and base64.b64decode(body["signature"]) == recs[3]["signature"]
+    assert base64.b64decode(body["randomness"]) == hashlib.sha256(recs[3]["signature"]).digest()
+    assert marshal_random_data({"round": 0, "signature": b"\x01"}) == b'{"signature":"AQ=="}'
