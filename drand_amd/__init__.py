@@ -13,5 +13,6 @@ from .scheme import (  # noqa: F401
     UNCHAINED_SCHEME,
     SHORT_SIG_SCHEME,
     SIGS_ON_G1_SCHEME,
+    hash_to_curve,
 )
 from .chain import Beacon, randomness_from_signature  # noqa: F401

@@ -43,6 +43,7 @@ SIGNATURES = {
     "dh_public_key": (_c.c_int, [_c.c_int, _c.c_char_p, _P]),
     "dh_partial_bytes": (_c.c_int, [_c.c_int]),
     "dh_set_split": (_c.c_int, [_c.c_uint64, _c.c_int]),
+    "dh_hash_to_curve": (_c.c_int, [_c.c_int, _P, _P, _c.c_size_t, _c.c_char_p, _c.c_size_t, _P]),
     "dh_batch_begin": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_size_t, _P, _P, _c.c_size_t, _P, _c.c_size_t, _P,
                                   _c.c_size_t, _P, _P, _c.c_uint64, _P, _c.POINTER(_P), _P]),
     "dh_check_partials": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_size_t, _P, _c.c_size_t, _c.POINTER(_c.c_int)]),

@@ -625,172 +625,6 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   return DH_OK;
 }
 
-// ---- scalar field F_r on the host (Lagrange coefficients; 4 x 64-bit Montgomery, R = 2^256)
-struct fr {
-  uint64_t v[4];
-};
-const uint64_t FR_R[4] = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL, 0x73eda753299d7d48ULL};
-const uint64_t FR_N0 = 0xfffffffeffffffffULL;  // -r^-1 mod 2^64
-typedef unsigned __int128 u128;
-
-bool fr_geq(const uint64_t* a, const uint64_t* b) {
-  for (int i = 3; i >= 0; i--) {
-    if (a[i] != b[i]) return a[i] > b[i];
-  }
-  return true;
-}
-void fr_subr(uint64_t* a) {
-  u128 br = 0;
-  for (int i = 0; i < 4; i++) {
-    u128 d = (u128)a[i] - FR_R[i] - br;
-    a[i] = (uint64_t)d;
-    br = (d >> 64) & 1;
-  }
-}
-fr fr_mul(const fr& a, const fr& b) {
-  uint64_t t[6] = {0};
-  for (int i = 0; i < 4; i++) {
-    u128 c = 0;
-    for (int j = 0; j < 4; j++) {
-      c += (u128)a.v[j] * b.v[i] + t[j];
-      t[j] = (uint64_t)c;
-      c >>= 64;
-    }
-    u128 s2 = (u128)t[4] + c;
-    t[4] = (uint64_t)s2;
-    t[5] = (uint64_t)(s2 >> 64);
-    uint64_t m = t[0] * FR_N0;
-    c = (u128)m * FR_R[0] + t[0];
-    c >>= 64;
-    for (int j = 1; j < 4; j++) {
-      c += (u128)m * FR_R[j] + t[j];
-      t[j - 1] = (uint64_t)c;
-      c >>= 64;
-    }
-    s2 = (u128)t[4] + c;
-    t[3] = (uint64_t)s2;
-    t[4] = t[5] + (uint64_t)(s2 >> 64);
-  }
-  fr r;
-  memcpy(r.v, t, 32);
-  if (t[4] || fr_geq(r.v, FR_R)) fr_subr(r.v);
-  return r;
-}
-fr fr_from_u64(uint64_t x) {  // Montgomery form of a small integer
-  static fr r2;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    uint64_t t[4] = {1, 0, 0, 0};
-    for (int i = 0; i < 512; i++) {  // 2^512 mod r by doubling
-      uint64_t c = 0;
-      for (int k = 0; k < 4; k++) {
-        uint64_t nv = (t[k] << 1) | c;
-        c = t[k] >> 63;
-        t[k] = nv;
-      }
-      if (c || fr_geq(t, FR_R)) fr_subr(t);
-    }
-    memcpy(r2.v, t, 32);
-  });
-  fr a = {{x, 0, 0, 0}};
-  return fr_mul(a, r2);
-}
-fr fr_sub(const fr& a, const fr& b) {
-  fr r;
-  u128 br = 0;
-  for (int i = 0; i < 4; i++) {
-    u128 d = (u128)a.v[i] - b.v[i] - br;
-    r.v[i] = (uint64_t)d;
-    br = (d >> 64) & 1;
-  }
-  if (br) {
-    u128 c = 0;
-    for (int i = 0; i < 4; i++) {
-      c += (u128)r.v[i] + FR_R[i];
-      r.v[i] = (uint64_t)c;
-      c >>= 64;
-    }
-  }
-  return r;
-}
-fr fr_inv(const fr& a) {  // a^(r-2)
-  uint64_t e[4];
-  memcpy(e, FR_R, 32);
-  e[0] -= 2;
-  fr acc = fr_from_u64(1);
-  for (int i = 255; i >= 0; i--) {
-    acc = fr_mul(acc, acc);
-    if ((e[i >> 6] >> (i & 63)) & 1) acc = fr_mul(acc, a);
-  }
-  return acc;
-}
-void fr_to_words(const fr& a, uint32_t out[8]) {  // leave Montgomery form, little-endian 32-bit words
-  fr one = {{1, 0, 0, 0}};
-  fr p = fr_mul(a, one);
-  for (int i = 0; i < 4; i++) {
-    out[2 * i] = (uint32_t)p.v[i];
-    out[2 * i + 1] = (uint32_t)(p.v[i] >> 32);
-  }
-}
-// non-adjacent form of a < 2^255 (little-endian 32-bit words): positive-digit mask, negative-digit mask
-// (256 positions each): ~1/3 of the positions are nonzero instead of ~1/2 of the bits
-static void naf_masks(const uint32_t w[8], uint32_t pos[8], uint32_t neg[8]) {
-  uint64_t k[5] = {0, 0, 0, 0, 0};
-  for (int i = 0; i < 4; i++) k[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
-  memset(pos, 0, 32);
-  memset(neg, 0, 32);
-  for (int b = 0; b < 257; b++) {
-    if (k[0] & 1) {
-      const bool minus = (k[0] & 3) == 3;  // digit -1: k += 1, else digit +1: k -= 1
-      if (b >= 256) break;                 // cannot happen for a < 2^255
-      if (minus) {
-        neg[b >> 5] |= 1u << (b & 31);
-        for (int i = 0; i < 5 && ++k[i] == 0; i++) {
-        }
-      } else {
-        pos[b >> 5] |= 1u << (b & 31);
-        k[0] -= 1;
-      }
-    }
-    for (int i = 0; i < 4; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 63);
-    k[4] >>= 1;
-  }
-}
-
-// Lagrange basis at 0 over x_k = idx_k + 1 (share.RecoverCommit / lagrangeBasis [kyber v1.1.18 share/poly.go]),
-// each coefficient as NAF masks: out[16 k .. 16 k + 7] positive digits, out[16 k + 8 .. 16 k + 15] negative
-void lagrange_at_zero(const std::vector<uint32_t>& idx, uint32_t* out /* t x 16 words */) {
-  const size_t t = idx.size();
-  std::vector<fr> den(t), num(t);
-  for (size_t k = 0; k < t; k++) {
-    fr xk = fr_from_u64((uint64_t)idx[k] + 1);
-    fr n = fr_from_u64(1), d = fr_from_u64(1);
-    for (size_t m = 0; m < t; m++) {
-      if (m == k) continue;
-      fr xm = fr_from_u64((uint64_t)idx[m] + 1);
-      n = fr_mul(n, xm);
-      d = fr_mul(d, fr_sub(xm, xk));
-    }
-    num[k] = n;
-    den[k] = d;
-  }
-  // batch inversion of the denominators
-  std::vector<fr> pre(t);
-  fr acc = fr_from_u64(1);
-  for (size_t k = 0; k < t; k++) {
-    pre[k] = acc;
-    acc = fr_mul(acc, den[k]);
-  }
-  fr inv = fr_inv(acc);
-  for (size_t k = t; k-- > 0;) {
-    fr dk_inv = fr_mul(inv, pre[k]);
-    inv = fr_mul(inv, den[k]);
-    uint32_t wds[8];
-    fr_to_words(fr_mul(num[k], dk_inv), wds);
-    naf_masks(wds, out + 16 * k, out + 16 * k + 8);
-  }
-}
-
 int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
                  const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* sig_out, uint8_t* status_out,
                  hipStream_t st, uint8_t* partial_ok_out = nullptr) {
@@ -1520,6 +1354,45 @@ int dh_sign_batch(int scheme, const uint8_t* sk32, const uint64_t* rounds, const
                           chained && prev_lens ? w->in_prev_lens.as<uint32_t>() : nullptr, nullptr, n, chained ? 1 : 0,
                           dst_id(scheme), w->in_sigs.as<uint8_t>(), w->q_pts.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), st));
   HIP_TRY(hipMemcpyAsync(sigs_out, w->in_sigs.p, n * sl, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return DH_OK;
+}
+
+int dh_hash_to_curve(int group, const uint8_t* msgs, const uint32_t* msg_off, size_t n, const uint8_t* dst, size_t dst_len,
+                     uint8_t* out) {
+  if (group != 1 && group != 2) return fail(DH_EINVAL, "group must be 1 (G1) or 2 (G2)");
+  if (!msg_off || !out || (n && !msgs) || !dst || dst_len == 0 || dst_len > 255)
+    return fail(DH_EINVAL, "bad hash_to_curve arguments (DST must be 1..255 bytes)");
+  if (n == 0) return DH_OK;
+  size_t maxm = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (msg_off[i + 1] < msg_off[i]) return fail(DH_EINVAL, "msg_off must be non-decreasing");
+    maxm = std::max<size_t>(maxm, msg_off[i + 1] - msg_off[i]);
+  }
+  const size_t total = msg_off[n] - msg_off[0];
+  const size_t stride = (64 + maxm + 4 + dst_len + 63) & ~(size_t)63;
+  const size_t outlen = group == 1 ? 48 : 96;
+  std::vector<uint32_t> off(n + 1);
+  for (size_t i = 0; i <= n; i++) off[i] = msg_off[i] - msg_off[0];
+  lease L;
+  if (L.rc) return L.rc;
+  worker* w = L.w;
+  int rc = set_device_and_stream(w);
+  if (rc) return rc;
+  hipStream_t st = w->stream;
+  HIP_TRY(w->in_sigs.ensure(total + 4));
+  HIP_TRY(w->in_prev_lens.ensure((n + 1) * 4));
+  HIP_TRY(w->key_raw.ensure(256));
+  HIP_TRY(w->h2c_tmp.ensure(n * stride));
+  HIP_TRY(w->out_rand.ensure(n * outlen));
+  if (total) HIP_TRY(hipMemcpyAsync(w->in_sigs.p, msgs + msg_off[0], total, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->in_prev_lens.p, off.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(w->key_raw.p, dst, dst_len, hipMemcpyHostToDevice, st));
+  w->cached_key_len = 0;  // key_raw reused as the DST buffer
+  HIP_TRY(dh::launch_h2c_generic(group == 2, w->in_sigs.as<uint8_t>(), w->in_prev_lens.as<uint32_t>(), n,
+                                 w->key_raw.as<uint8_t>(), (uint32_t)dst_len, w->h2c_tmp.as<uint8_t>(), stride,
+                                 w->out_rand.as<uint8_t>(), st));
+  HIP_TRY(hipMemcpyAsync(out, w->out_rand.p, n * outlen, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   return DH_OK;
 }

@@ -139,16 +139,19 @@ DH_DEV bool jac_add_distinct(jac<F>& r, const jac<F>& p, const jac<F>& q) {
 // The isogeny is a group homomorphism, so Q = iso(swu(u0) + swu(u1)): the two SSWU points are added on E1'
 // and ONE isogeny is evaluated (~117 products saved per round). Same point, same bytes. When the two SSWU
 // points share x (never for honest inputs) the textbook order is used: two isogenies, addition on E1.
-DH_DEV jac<fp> h2c_g1_noclear(const sha_h& digest, int dst_id) {
-  uint32_t b[4][8];
-  xmd32<4>(b, digest, dst_id);
-  fp u0 = fp_from_be512(b[0], b[1]);
-  fp u1 = fp_from_be512(b[2], b[3]);
+// map_to_curve of two field elements, summed (hash_to_curve minus the hashing and the cofactor clearing)
+DH_DEV jac<fp> h2c_g1_map(const fp& u0, const fp& u1) {
   const jac<fp> p0 = swu_jac(sswu_g1(u0));
   const jac<fp> p1 = swu_jac(sswu_g1(u1));
   jac<fp> s;
   if (jac_add_distinct(s, p0, p1)) return iso11_jac(s);
   return jac_add(iso11_jac(p0), iso11_jac(p1));
+}
+
+DH_DEV jac<fp> h2c_g1_noclear(const sha_h& digest, int dst_id) {
+  uint32_t b[4][8];
+  xmd32<4>(b, digest, dst_id);
+  return h2c_g1_map(fp_from_be512(b[0], b[1]), fp_from_be512(b[2], b[3]));
 }
 
 // clear_cofactor(G1) = [h_eff] P, h_eff = 1 - u = 0xd201000000010001 = |u| + 1
@@ -246,16 +249,18 @@ DH_DEV jac<fp2> iso3_jac_lean(const jac<fp2>& p) {
 }
 
 // hash_to_curve(G2) without clear_cofactor, one isogeny after the addition on E2' (see h2c_g1_noclear)
-DH_DEV jac<fp2> h2c_g2_noclear(const sha_h& digest, int dst_id) {
-  uint32_t b[8][8];
-  xmd32<8>(b, digest, dst_id);
-  fp2 u0 = {fp_from_be512(b[0], b[1]), fp_from_be512(b[2], b[3])};
-  fp2 u1 = {fp_from_be512(b[4], b[5]), fp_from_be512(b[6], b[7])};
+DH_DEV jac<fp2> h2c_g2_map(const fp2& u0, const fp2& u1) {
   const jac<fp2> p0 = swu_jac(sswu_g2(u0));
   const jac<fp2> p1 = swu_jac(sswu_g2(u1));
   jac<fp2> s;
   if (jac_add_distinct(s, p0, p1)) return iso3_jac(s);
   return jac_add(iso3_jac(p0), iso3_jac(p1));
+}
+
+DH_DEV jac<fp2> h2c_g2_noclear(const sha_h& digest, int dst_id) {
+  uint32_t b[8][8];
+  xmd32<8>(b, digest, dst_id);
+  return h2c_g2_map({fp_from_be512(b[0], b[1]), fp_from_be512(b[2], b[3])}, {fp_from_be512(b[4], b[5]), fp_from_be512(b[6], b[7])});
 }
 
 // psi (untwist-Frobenius-twist) on E2 and its square, Jacobian

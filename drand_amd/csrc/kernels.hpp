@@ -86,6 +86,9 @@ hipError_t launch_multi_pairing_vm(const uint32_t* P, const uint32_t* Q, size_t 
 hipError_t launch_sign(int sig_g2, const uint32_t* sk, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride,
                        const uint32_t* prev_lens, const uint8_t* msgs32, size_t n, int chained, int dst_id, uint8_t* out,
                        uint32_t* q_tmp, uint32_t* h_tmp, hipStream_t st);
+// RFC 9380 hash_to_curve of arbitrary messages / DST, compressed (k_sign.hip)
+hipError_t launch_h2c_generic(int g2, const uint8_t* msgs, const uint32_t* off, size_t n, const uint8_t* dst, uint32_t dlen,
+                              uint8_t* scratch, size_t sstride, uint8_t* out, hipStream_t st);
 hipError_t launch_pubkey(int key_g2, const uint32_t* sk, uint8_t* out, hipStream_t st);
 
 // tbls Recover (k_recover.hip)

@@ -175,6 +175,31 @@ DH_DEV sha_h digest_chained_any(const uint8_t* prev, uint32_t prevlen, uint64_t 
   return s;
 }
 
+// SHA-256 of len bytes at p (any alignment), one compression per 64 bytes
+DH_DEV sha_h sha256_bytes(const uint8_t* p, uint64_t len) {
+  const uint64_t nb = (len + 9 + 63) >> 6;
+  sha_h s = sha_iv();
+#pragma unroll 1
+  for (uint64_t blk = 0; blk < nb; blk++) {
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint64_t pos = blk * 64 + (uint64_t)(4 * j + b);
+        const uint32_t byte = pos < len ? p[pos] : (pos == len ? 0x80u : 0u);
+        v = (v << 8) | byte;
+      }
+      if (blk == nb - 1 && j == 14) v = (uint32_t)((len * 8) >> 32);
+      if (blk == nb - 1 && j == 15) v = (uint32_t)(len * 8);
+      w[j] = v;
+    }
+    sha_compress(s, w);
+  }
+  return s;
+}
+
 // expand_message_xmd(SHA-256, msg = 32-byte digest, DST = 43 bytes, len = 32*NOUT):
 // writes NOUT 32-byte blocks b_1..b_NOUT (as big-endian words) into out[NOUT][8].
 // dst_id 0 = G2 DST, 1 = G1 DST; len_id 0 = 128 bytes (hash to G1), 1 = 256 bytes (G2).

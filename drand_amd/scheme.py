@@ -305,6 +305,19 @@ _SCHEMES = {
 }
 
 
+def hash_to_curve(group, messages, dst):
+    """RFC 9380 hash_to_curve on the device: group 1 (G1) or 2 (G2), a list of byte strings, one DST. Returns the
+    compressed points (list of bytes)."""
+    msgs = [bytes(m) for m in messages]
+    off = np.zeros(len(msgs) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    blob = np.frombuffer(b"".join(msgs) or b"\0", dtype=np.uint8).copy()
+    size = 48 if group == 1 else 96
+    out = np.zeros((len(msgs), size), dtype=np.uint8)
+    _check(_lib.load().dh_hash_to_curve(int(group), _ptr(blob), _ptr(off), len(msgs), bytes(dst), len(dst), _ptr(out)))
+    return [r.tobytes() for r in out]
+
+
 def scheme_from_name(name):
     """crypto.SchemeFromName; raises SchemeError("invalid scheme name '...'")."""
     try:

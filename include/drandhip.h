@@ -178,6 +178,16 @@ int dh_sign_batch(int scheme, const uint8_t* sk32, const uint64_t* rounds, const
 int dh_public_key(int scheme, const uint8_t* sk32, uint8_t* key_out);
 
 /*
+ * RFC 9380 hash_to_curve (random-oracle encoding, expand_message_xmd with SHA-256) on the device for n arbitrary
+ * messages (message i = msgs[msg_off[i] .. msg_off[i+1])) under one DST of 1..255 bytes: group 1 = G1 (SSWU on the
+ * 11-isogenous curve), group 2 = G2 (3-isogenous). out: n compressed points (48 / 96 bytes). The general form of the
+ * fixed-shape hashing inside the batch kernels (kilic HashToCurve as used by kyber-bls12381's Hash, [ext]); pinned
+ * by the RFC 9380 J.9.1 / J.10.1 vectors in tests/kat.py.
+ */
+int dh_hash_to_curve(int group, const uint8_t* msgs, const uint32_t* msg_off, size_t n, const uint8_t* dst, size_t dst_len,
+                     uint8_t* out);
+
+/*
  * Live kernel timing: when enabled, every device stage of the verification path is bracketed by HIP
  * events on the stream it is launched on; dh_profile_read writes a JSON object
  * {"stage": {"count": c, "total_ms": t}, ...} into buf (returns the full length). dh_profile resets.

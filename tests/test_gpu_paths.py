@@ -434,3 +434,31 @@ def test_node_wide_check_protocol(dh):
     assert stats[0][1] == 0 and stats[1][1] >= 1  # the clean shard passed its own level-0 check
     ref, _ = s.verify_beacons(pk, rounds, bad, seed=5)
     assert np.array_equal(ref, v.astype(bool))
+
+
+# ---------------------------------------------------------------- RFC 9380 hash_to_curve on the device
+def test_hash_to_curve_rfc9380_device(dh):
+    """dh_hash_to_curve (arbitrary message and DST) reproduces the RFC 9380 J.9.1 (G1) / J.10.1 (G2) vectors exactly
+    — the quicknet hash path up to its DST — and agrees with the batch kernels' fixed-shape hashing on the drand
+    DSTs (hash of a 32-byte digest, as in a signature of the device signer)."""
+    import bls_py
+    from kat import H2C_DST_G1, H2C_DST_G2, H2C_G1, H2C_G2
+    pts = dh.hash_to_curve(1, [m for m, _, _ in H2C_G1], H2C_DST_G1)
+    for (m, x, y), c in zip(H2C_G1, pts):
+        assert bls_py.g1_decompress(c) == (int(x, 16), int(y, 16)), m[:8]
+    pts = dh.hash_to_curve(2, [v[0] for v in H2C_G2], H2C_DST_G2)
+    for (m, x0, x1, y0, y1), c in zip(H2C_G2, pts):
+        (px0, px1), (py0, py1) = bls_py.g2_decompress(c)
+        assert (px0, px1, py0) == (int(x0, 16), int(x1, 16), int(y0, 16)), m
+        if y1 is not None:
+            assert py1 == int(y1, 16)
+    # [1] H(m) from the signer = H(m) of the generic path, for both drand DSTs
+    one = (1).to_bytes(32, "big")
+    for name, group, dst in (("bls-unchained-g1-rfc9380", 1, b"BLS_SIG_BLS12381G1_XMD:SHA-256_SSWU_RO_NUL_"),
+                             ("bls-unchained-on-g1", 1, b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_"),
+                             ("pedersen-bls-unchained", 2, b"BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_")):
+        s = dh.scheme_from_name(name)
+        rounds = np.array([1, 77, 2 ** 40 + 3], dtype=np.uint64)
+        sig = s.sign_beacons(one, rounds)
+        gen = dh.hash_to_curve(group, [s.digest_beacon(int(r)) for r in rounds], dst)
+        assert [x.tobytes() for x in sig] == gen, name

@@ -79,3 +79,18 @@ def test_golden_replay(oracle):
     faulty = [r for r, s, p in zip(rp["rounds"], stored, prevs)
               if not oracle.verify_beacon("pedersen-bls-chained", pk, r, s, p)]
     assert faulty == rp["faulty"] == [10, 11]
+
+
+def test_hash_to_curve_rfc9380_vectors(oracle):
+    """RFC 9380 J.9.1 (G1) and J.10.1 (G2) vectors: the oracle's hash_to_curve with the QUUX test DSTs. With the
+    quicknet DST this is the whole quicknet hash path, so quicknet is pinned up to its DST string."""
+    import bls_py
+    from kat import H2C_DST_G1, H2C_DST_G2, H2C_G1, H2C_G2
+    for msg, x, y in H2C_G1:
+        pt = bls_py.g1_decompress(oracle.hash_to_curve(False, msg, H2C_DST_G1))
+        assert pt == (int(x, 16), int(y, 16)), msg[:8]
+    for msg, x0, x1, y0, y1 in H2C_G2:
+        (px0, px1), (py0, py1) = bls_py.g2_decompress(oracle.hash_to_curve(True, msg, H2C_DST_G2))
+        assert (px0, px1, py0) == (int(x0, 16), int(x1, 16), int(y0, 16)), msg
+        if y1 is not None:
+            assert py1 == int(y1, 16)
