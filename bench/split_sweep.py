@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=1 << 20)
     ap.add_argument("--calls", type=int, default=4)
     ap.add_argument("--scheme", default="bls-unchained-g1-rfc9380")
-    ap.add_argument("--grid", default="0x1,262144x4,262144x8,131072x8,65536x8,32768x8,65536x12,32768x16")
+    ap.add_argument("--grid", default="0x1,262144x3,262144x2,131072x3,131072x2,196608x3,524288x2")
     args = ap.parse_args()
     import torch
     from drand_amd import _lib, scheme_from_name

@@ -22,6 +22,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cmath>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -461,10 +462,20 @@ enum verify_mode {
   VM_FINISH_PASS = 3  // after VM_BEGIN, the node-wide check passed: every decoded round is valid
 };
 
+// One-call pipelining (run_split): the per-round kernels of consecutive chunks run one after another, each chunk's
+// alone on the chip, while the latency-bound tails of earlier chunks (MSM reduction, pairing checks) run beside
+// them on their own streams. A chunk's per-round kernels wait for the previous chunk's (an event), and it records
+// its own event once they are queued.
+struct prep_gate {
+  hipEvent_t wait = nullptr;  // the previous chunk's per-round kernels (null: first chunk)
+  hipEvent_t done = nullptr;  // this chunk's
+  std::function<void()> recorded;  // host side: `done` is recorded, the next chunk may queue behind it
+};
+
 int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                 size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
                 uint8_t* d_verdict, uint8_t* d_rand, uint64_t seed, hipStream_t st, uint64_t* stats,
-                const uint8_t* d_msgs32 = nullptr, int mode = VM_FULL) {
+                const uint8_t* d_msgs32 = nullptr, int mode = VM_FULL, prep_gate* gate = nullptr) {
   const bool g2 = sig_on_g2(scheme);
   const int sig_len = g2 ? 96 : 48, key_len = g2 ? 48 : 96;
   if ((int)pk_len != key_len) return fail(DH_EINVAL, "public key must be %d bytes for scheme %d", key_len, scheme);
@@ -499,6 +510,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(w->q_pts.ensure(n * jw * 4));
     HIP_TRY(w->scal.ensure(n * 16));
     HIP_TRY(w->entries.ensure(n * 4));
+    if (gate && gate->wait) HIP_TRY(hipStreamWaitEvent(st, gate->wait, 0));
     HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>" : "k_prep_sig<fp>", [&] {
       return dh::launch_prep(g2, d_sigs, sig_stride, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), d_rand, st);
     }));
@@ -517,6 +529,10 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
     HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), st));
     HIP_TRY(hipMemsetAsync(d_verdict, 0, n, st));
+    if (gate) {
+      HIP_TRY(hipEventRecord(gate->done, st));
+      gate->recorded();
+    }
     HIP_TRY(hipStreamSynchronize(st));
     if (!key_hit) {
       memcpy(w->cached_key, pk, pk_len);
@@ -855,15 +871,18 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
 }
 
 // ---- one call over many internal streams (the drop-in callers make ONE call per window)
-// A batch of n rounds is cut into chunks verified concurrently by up to `workers` leased workers (each its own
-// HIP stream and workspace), so a single dh_verify_batch gets the overlap the bench gets from several calls in
-// flight: one chunk's latency-bound group check runs beside the next chunk's per-round kernels. Every chunk is
-// a complete batch check (its own RLC scalars: seed + chunk index when the caller fixed a seed, fresh CSPRNG
-// seeds otherwise), so verdicts stay bit-exact per round. DRANDHIP_SPLIT="chunk,workers" overrides the
-// defaults (262144 rounds, 8 workers); "0" disables splitting.
+// A batch of n rounds is cut into chunks verified by up to `workers` leased workers (each its own HIP stream and
+// workspace). The chunks' per-round kernels are chained in chunk order across the streams (prep_gate), so each
+// runs alone at the chip's full rate, while earlier chunks' MSMs and latency-bound group checks run beside them:
+// the call costs about the sum of the per-round kernels plus ONE chunk's tail. Streams map onto the process's
+// hardware queues (GPU_MAX_HW_QUEUES, 4 by default, one of them usually held by the caller's own stream), and two
+// streams on one queue run in order, so a tail would block the next chunk's kernels: 3 workers by default. Every
+// chunk is a complete batch check (its own RLC scalars: seed + chunk index when the caller fixed a seed, fresh
+// CSPRNG seeds otherwise), so verdicts stay bit-exact per round. DRANDHIP_SPLIT="chunk,workers" overrides the
+// defaults (262144 rounds, 3 workers); "0" disables splitting.
 struct split_cfg {
   size_t chunk = 262144;
-  int workers = 8;
+  int workers = 3;
 };
 std::mutex g_split_mu;
 split_cfg g_split = [] {
@@ -900,13 +919,42 @@ int run_split(size_t n, F&& fn, uint64_t seed) {
   std::atomic<int> first_rc{DH_OK};
   std::mutex err_mu;
   std::string err;
+  // prep chain: chunk c's per-round kernels queue behind chunk c-1's (event ev[c-1], recorded by its thread)
+  std::vector<hipEvent_t> ev(nchunks > 1 ? nchunks : 0, nullptr);
+  std::vector<char> rec(nchunks, 0);
+  std::mutex gate_mu;
+  std::condition_variable gate_cv;
+  for (auto& e : ev) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      for (auto& x : ev)
+        if (x) (void)hipEventDestroy(x);
+      return fail(DH_EDEVICE, "hipEventCreate failed");
+    }
+  }
+  auto mark = [&](size_t c) {
+    std::lock_guard<std::mutex> lk(gate_mu);
+    rec[c] = 1;
+    gate_cv.notify_all();
+  };
   auto body = [&]() {
     lease L;
     int rc = L.rc ? L.rc : set_device_and_stream(L.w);
     for (size_t c; !rc && (c = next.fetch_add(1)) < nchunks;) {
       const size_t lo = c * per, hi = std::min(n, lo + per);
-      if (lo >= hi) continue;
-      rc = fn(L.w, lo, hi, seed ? seed + 0x9e3779b97f4a7c15ULL * c : 0);
+      prep_gate g;
+      prep_gate* gp = nullptr;
+      if (nchunks > 1) {
+        if (c > 0) {  // chunk c-1 is held by a running thread that never waits on a later chunk: no deadlock
+          std::unique_lock<std::mutex> lk(gate_mu);
+          gate_cv.wait(lk, [&] { return rec[c - 1] != 0; });
+          g.wait = ev[c - 1];
+        }
+        g.done = ev[c];
+        g.recorded = [&mark, c] { mark(c); };
+        gp = &g;
+      }
+      if (lo < hi) rc = fn(L.w, lo, hi, seed ? seed + 0x9e3779b97f4a7c15ULL * c : 0, gp);
+      if (nchunks > 1) mark(c);  // also on failure: the next chunk must not wait forever
     }
     if (rc) {
       int expect = DH_OK;
@@ -925,6 +973,7 @@ int run_split(size_t n, F&& fn, uint64_t seed) {
     body();
     for (auto& th : ths) th.join();
   }
+  for (auto& e : ev) (void)hipEventDestroy(e);
   const int rc = first_rc.load();
   if (rc) g_err = err;
   return rc;
@@ -989,14 +1038,15 @@ int dh_verify_batch_device(int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(hipEventRecord(ready, (hipStream_t)hip_stream));
   }
   std::mutex stats_mu;
-  int rc = run_split(n, [&](worker* w, size_t lo, size_t hi, uint64_t chunk_seed) -> int {
+  int rc = run_split(n, [&](worker* w, size_t lo, size_t hi, uint64_t chunk_seed, prep_gate* gate) -> int {
     if (ready) HIP_TRY(hipStreamWaitEvent(w->stream, ready, 0));
     uint64_t st4[4];
     const bool chained = scheme == DH_SCHEME_CHAINED && d_prevs;
     int r = verify_core(w, scheme, pk, pk_len, d_rounds + lo, d_sigs + lo * sig_stride, sig_stride,
                         chained ? d_prevs + lo * prev_stride : nullptr,
                         prev_stride, chained && d_prev_lens ? d_prev_lens + lo : nullptr, hi - lo, d_verdict_out + lo,
-                        d_rand_out ? d_rand_out + lo * 32 : nullptr, chunk_seed, w->stream, stats_out ? st4 : nullptr);
+                        d_rand_out ? d_rand_out + lo * 32 : nullptr, chunk_seed, w->stream, stats_out ? st4 : nullptr,
+                        nullptr, VM_FULL, gate);
     if (!r && stats_out) {
       std::lock_guard<std::mutex> lk(stats_mu);
       stats_out[0] = std::max(stats_out[0], st4[0]);
@@ -1020,7 +1070,7 @@ int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t
       if (prev_lens[i] > prev_stride)
         return fail(DH_EINVAL, "previous signature %zu: length %u exceeds the record stride %zu", i, prev_lens[i], prev_stride);
   // one chunk per worker at a time: its host->device copies overlap the other chunks' kernels
-  return run_split(n, [&](worker* w, size_t lo, size_t hi, uint64_t chunk_seed) -> int {
+  return run_split(n, [&](worker* w, size_t lo, size_t hi, uint64_t chunk_seed, prep_gate* gate) -> int {
     const size_t m = hi - lo;
     hipStream_t st = w->stream;
     HIP_TRY(w->in_rounds.ensure(m * 8));
@@ -1040,7 +1090,7 @@ int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t
     int rc = verify_core(w, scheme, pk, pk_len, w->in_rounds.as<uint64_t>(), w->in_sigs.as<uint8_t>(), sig_stride,
                          chained ? w->in_prevs.as<uint8_t>() : nullptr, prev_stride,
                          chained && prev_lens ? w->in_prev_lens.as<uint32_t>() : nullptr, m, w->out_verdict.as<uint8_t>(),
-                         rand_out ? w->out_rand.as<uint8_t>() : nullptr, chunk_seed, st, nullptr);
+                         rand_out ? w->out_rand.as<uint8_t>() : nullptr, chunk_seed, st, nullptr, nullptr, VM_FULL, gate);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(verdict_out + lo, w->out_verdict.p, m, hipMemcpyDeviceToHost, st));
     if (rand_out) HIP_TRY(hipMemcpyAsync(rand_out + lo * 32, w->out_rand.p, m * 32, hipMemcpyDeviceToHost, st));

@@ -312,16 +312,18 @@ DH_DEV fp fp_pow_words(const fp& x, const uint32_t* e, int nbits) {
 // x^e for a fixed exponent given as a sliding-window schedule (consts.hpp SCHED_*, w = 3):
 // table x, x^3, x^5, x^7; sched[0] = first table index, then (squarings << 8 | index), index 0xff =
 // squarings only. 378 squarings + ~105 multiplications for the 381-bit exponents (binary: ~228).
-DH_DEV fp fp_pow_sched(const fp& x, const uint16_t* sched, int len) {
+DH_DEV fp fp_pow_sched(const fp& x, const uint32_t* sched, int len) {
   const fp x2 = fp_sqr(x);
   const fp t1 = fp_mul(x, x2);
   const fp t2 = fp_mul(t1, x2);
   const fp t3 = fp_mul(t2, x2);
   auto pick = [&](uint32_t k) { return k == 0 ? x : (k == 1 ? t1 : (k == 2 ? t2 : t3)); };
   fp acc = pick(sched[0]);
+  uint32_t next = sched[1];  // the tables end with a 0 entry: the read one step ahead stays in bounds
 #pragma unroll 1
   for (int i = 1; i < len; i++) {
-    const uint32_t op = sched[i];
+    const uint32_t op = next;
+    next = sched[i + 1];  // scalar load issued a whole step before its use
     const uint32_t nsq = op >> 8, k = op & 0xff;
 #pragma unroll 1
     for (uint32_t j = 0; j < nsq; j++) acc = fp_sqr(acc);

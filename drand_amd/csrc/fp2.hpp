@@ -69,16 +69,18 @@ DH_DEV fp2 fp2_pow_small(const fp2& x, uint32_t e) {
 }
 
 // x^e for a fixed exponent given as a sliding-window schedule (w = 3, see fp_pow_sched)
-DH_DEV fp2 fp2_pow_sched(const fp2& x, const uint16_t* sched, int len) {
+DH_DEV fp2 fp2_pow_sched(const fp2& x, const uint32_t* sched, int len) {
   const fp2 x2 = fp2_sqr(x);
   const fp2 t1 = fp2_mul(x, x2);
   const fp2 t2 = fp2_mul(t1, x2);
   const fp2 t3 = fp2_mul(t2, x2);
   auto pick = [&](uint32_t k) { return k == 0 ? x : (k == 1 ? t1 : (k == 2 ? t2 : t3)); };
   fp2 acc = pick(sched[0]);
+  uint32_t next = sched[1];  // the tables end with a 0 entry: the read one step ahead stays in bounds
 #pragma unroll 1
   for (int i = 1; i < len; i++) {
-    const uint32_t op = sched[i];
+    const uint32_t op = next;
+    next = sched[i + 1];  // scalar load issued a whole step before its use
     const uint32_t nsq = op >> 8, k = op & 0xff;
 #pragma unroll 1
     for (uint32_t j = 0; j < nsq; j++) acc = fp2_sqr(acc);

@@ -42,6 +42,38 @@ __global__ __launch_bounds__(256, occ<F>::W) void k_prep_sig(const uint8_t* __re
   st_aff_aos<F>(sig_aff, i, a);
 }
 
+// G2 signatures in two passes: decompression (Fp2 square root) and the psi subgroup test each fit one lane's
+// registers, the fused kernel spilled 1.1 KB per lane. The affine point and status go through HBM between them
+// (96 + 1 B per round, written and read once).
+__global__ __launch_bounds__(256, occ<fp2>::W) void k_dec_sig_g2(const uint8_t* __restrict__ sigs, size_t stride, size_t n,
+                                                             uint8_t* __restrict__ status, uint32_t* __restrict__ sig_aff,
+                                                             uint8_t* __restrict__ rand_out) {
+  size_t i = gtid();
+  if (i >= n) return;
+  const uint8_t* s = sigs + i * stride;
+  aff<fp2> a;
+  uint8_t st = g2_decompress(a, s, false);
+  if (rand_out) st_digest(rand_out + 32 * i, sha256_aligned<96>(s));
+  if (st != DEC_OK) {
+    a.x = fp2{};
+    a.y = fp2{};
+    st = DEC_BAD;  // infinity signatures are rejected like kilic's engine + kyber's verify
+  }
+  status[i] = st;
+  st_aff_aos<fp2>(sig_aff, i, a);
+}
+
+__global__ __launch_bounds__(256, occ<fp2>::W) void k_sub_sig_g2(size_t n, uint8_t* __restrict__ status,
+                                                             uint32_t* __restrict__ sig_aff) {
+  size_t i = gtid();
+  if (i >= n || status[i] != DEC_OK) return;
+  const aff<fp2> a = ld_aff_aos<fp2>(sig_aff, i);
+  if (!g2_in_subgroup(a)) {
+    status[i] = DEC_BAD;
+    st_aff_aos<fp2>(sig_aff, i, aff<fp2>{fp2{}, fp2{}});
+  }
+}
+
 // ---------------------------------------------------------------- prep: messages -> hash points (no cofactor)
 // G1 (fused): hash_to_curve without clear_cofactor, one round per lane
 __global__ __launch_bounds__(256, occ<fp>::W) void k_prep_msg_g1(const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs,
@@ -154,9 +186,10 @@ __global__ void k_decode_key(const uint8_t* __restrict__ pk, uint32_t* __restric
 hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n, uint8_t* status, uint32_t* sig_aff,
                        uint8_t* rand_out, hipStream_t st) {
   if (!n) return hipSuccess;
-  if (sig_g2)
-    hipLaunchKernelGGL(k_prep_sig<fp2>, dim3(nblk(n, 256)), dim3(256), 0, st, sigs, stride, n, status, sig_aff, rand_out);
-  else
+  if (sig_g2) {
+    hipLaunchKernelGGL(k_dec_sig_g2, dim3(nblk(n, 256)), dim3(256), 0, st, sigs, stride, n, status, sig_aff, rand_out);
+    hipLaunchKernelGGL(k_sub_sig_g2, dim3(nblk(n, 256)), dim3(256), 0, st, n, status, sig_aff);
+  } else
     hipLaunchKernelGGL(k_prep_sig<fp>, dim3(nblk(n, 256)), dim3(256), 0, st, sigs, stride, n, status, sig_aff, rand_out);
   return hipGetLastError();
 }

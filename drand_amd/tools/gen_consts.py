@@ -351,7 +351,9 @@ def main():
                     ("SCHED_LEGENDRE", (P - 1) // 2), ("SCHED_SR2_C3", c3)):
         sched = window_schedule(e, 3)
         w("constexpr int %s_LEN = %d;" % (name, len(sched)))
-        w("__device__ __constant__ uint16_t %s[%d] = {%s};" % (name, len(sched), ", ".join("0x%04x" % v for v in sched)))
+        # 32-bit entries: a wave-uniform index into a dword table is a scalar (s_load) read; 16-bit entries can only
+        # be read by per-lane vector loads, whose latency each step of the chain then waits for
+        w("__device__ __constant__ uint32_t %s[%d] = {%s};" % (name, len(sched) + 1, ", ".join("0x%04x" % v for v in sched + [0])))
     w("constexpr uint32_t SR2_C4 = %du;" % c4)
     w("constexpr uint32_t SR2_C5 = %du;" % c5)
     w("constexpr int SR2_C1 = %d;" % c1)

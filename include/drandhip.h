@@ -75,8 +75,10 @@ int dh_key_len(int scheme);
  *   rand_out     n*32 bytes SHA-256(sig) (RandomnessFromSignature) or NULL
  *   seed         0 = draw the random-linear-combination seed from the OS CSPRNG; otherwise deterministic
  * One call uses several internal HIP streams for large n: the rounds are cut into chunks (262 144 rounds by
- * default) verified concurrently by up to 8 workers, each chunk a complete batch check, so one caller gets the
- * overlap of several batches in flight. DRANDHIP_SPLIT="chunk,workers" changes this ("0": one stream per call).
+ * default), each a complete batch check, verified by up to 3 workers; the chunks' per-round kernels run one
+ * after another at the chip's full rate while earlier chunks' MSMs and group checks run beside them, so a call
+ * costs about its per-round work plus one chunk's latency tail. DRANDHIP_SPLIT="chunk,workers" changes this
+ * ("0": one stream per call).
  * Returns DH_OK or a negative error code (no verdicts are valid on error).
  */
 int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* rounds, const uint8_t* sigs,
