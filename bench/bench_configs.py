@@ -318,7 +318,10 @@ def main():
     ap.add_argument("--subsets", choices=["first", "random"], default="first")
     ap.add_argument("--cpu-sample", type=int, default=2000)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--split", default="0", help="the library's one-call split (DRANDHIP_SPLIT): off, so each of the "
+                    "--streams batches in flight is one stream")
     args = ap.parse_args()
+    os.environ["DRANDHIP_SPLIT"] = args.split  # read when the library loads
     if args.config == "recover":
         args.rounds = args.rounds or 100000
         out = cfg_recover(args)

@@ -281,27 +281,33 @@ int make_seed(uint64_t seed, uint32_t words[8]) {
   return DH_OK;
 }
 
-// MSM geometry for groups of gsize rounds
-dh::msm_geom geom_for(size_t gsize) {
+// MSM geometry for groups of gsize rounds; glv: the endomorphism split (2 x gsize points, 63-bit scalar halves)
+dh::msm_geom geom_for(size_t gsize, bool glv = false) {
+  const size_t npts = glv ? 2 * gsize : gsize;
+  const int sbits = glv ? 63 : 127;  // scalar bits (k_scalars)
   int lg = 0;
-  while (((size_t)1 << (lg + 1)) <= gsize) lg++;
+  while (((size_t)1 << (lg + 1)) <= npts) lg++;
   int c = std::max(3, std::min(16, lg - 2));
-  // 127-bit scalars: keep the top window's t bits at >= c - 4, since each of its 2^(t-1) buckets collects
-  // ~m / 2^(t-1) entries and a bucket that spans many chunks is summed serially by k_msm_bucket_fix
-  // (c = 14 would leave t = 1: two buckets holding the whole set). Allowed: 16, 13, 10, 8, 5, 4, 3.
+  // keep the top window's t bits at >= c - 4, since each of its 2^(t-1) buckets collects ~m / 2^(t-1) entries
+  // and a bucket that spans many chunks is summed serially by k_msm_bucket_fix (127-bit scalars at c = 14 would
+  // leave t = 1: two buckets holding the whole set)
   while (c > 3) {
-    const int nw = (128 + c - 1) / c, t = 127 - c * (nw - 1);
+    const int nw = (sbits + 1 + c - 1) / c, t = sbits - c * (nw - 1);
     if (t >= c - 4) break;
     c--;
   }
   dh::msm_geom g;
   g.gsize = (uint32_t)gsize;
   g.c = c;
-  g.nwin = (128 + c - 1) / c;
+  g.nwin = (sbits + 1 + c - 1) / c;
   g.nbuck = (1u << (c - 1)) + 1;  // signed digits: |d| in [1, 2^(c-1)] (k_msm.hip: signed_digit)
-  uint32_t nseg = std::max(1u, std::min(2048u, g.nbuck / 32));
+  // bucket reduction: segments of ~8 digits, one thread each (k_msm_segsum): 16 additions + the segment's offset
+  // multiple per thread, then a log-depth tree
+  uint32_t nseg = std::max(1u, std::min(8192u, g.nbuck / 8));
   g.nseg = nseg;
   g.seglen = (g.nbuck - 1 + nseg - 1) / nseg;
+  g.halves = glv ? 2 : 1;
+  g.half_stride = 0;  // set by the caller: the point-array offset of the endomorphism images
   return g;
 }
 
@@ -420,7 +426,10 @@ static const std::vector<size_t>& fixed_ladder() {
 // latency floor), per-round leaf checks ~12 + 0.005 m. Faults are modelled as Poisson at the density the last
 // level observed (faulty groups -> -ln(1 - f) faults per group, at least one per failing group; when every
 // group failed, 5 per group). The next size minimises the expected cost of the rest of the descent.
-static double msm_cost_ms(double m, size_t g) { return 9.0 + 1.8e-6 * m * (double)geom_for(g).nwin; }
+static double msm_cost_ms(double m, size_t g) {
+  const dh::msm_geom gg = geom_for(g, true);
+  return 9.0 + 1.8e-6 * m * (double)(gg.nwin * gg.halves) / 2.0;  // fitted on 127-bit entries (8 per round at c = 16)
+}
 static double check_cost_ms(double groups) { return 12.0 + 0.0025 * groups; }
 static double leaf_cost_ms(double m) { return 12.0 + 0.005 * m; }
 
@@ -482,7 +491,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (sig_stride < (size_t)sig_len || sig_stride % 4) return fail(DH_EINVAL, "bad signature stride %zu", sig_stride);
   if (stats) memset(stats, 0, 4 * sizeof(uint64_t));
   if (n == 0) return DH_OK;
-  if (n >= 0x80000000u) return fail(DH_EINVAL, "batch too large");  // sorted-list entries keep a sign bit
+  // sorted-list entries keep a sign bit and address 2n points (the endomorphism images follow the n points)
+  if (n >= 0x40000000u) return fail(DH_EINVAL, "batch too large");
   const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
   const size_t aw = jw * 2 / 3;
 
@@ -506,8 +516,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
 
     // per-round prep
     HIP_TRY(w->status.ensure(n));
-    HIP_TRY(w->sig_aff.ensure(n * aw * 4));
-    HIP_TRY(w->q_pts.ensure(n * jw * 4));
+    HIP_TRY(w->sig_aff.ensure(2 * n * aw * 4));  // points i < n, then their endomorphism images (launch_endo)
+    HIP_TRY(w->q_pts.ensure(2 * n * jw * 4));
     HIP_TRY(w->scal.ensure(n * 16));
     HIP_TRY(w->entries.ensure(n * 4));
     if (gate && gate->wait) HIP_TRY(hipStreamWaitEvent(st, gate->wait, 0));
@@ -527,7 +537,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     if (rc) return rc;
     uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
     HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
-    HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), st));
+    HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), 1, st));
+    HIP_TRY(dh::launch_endo(g2, n, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(), st));
     HIP_TRY(hipMemsetAsync(d_verdict, 0, n, st));
     if (gate) {
       HIP_TRY(hipEventRecord(gate->done, st));
@@ -557,21 +568,22 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   int level = 0;
   while (m > 0 && gsize > 1) {
     gsize = std::min(gsize, m);
-    const dh::msm_geom g = geom_for(gsize);
+    dh::msm_geom g = geom_for(gsize, true);
+    g.half_stride = (uint32_t)n;
     const size_t ngroups = (m + gsize - 1) / gsize;
     const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
     HIP_TRY(w->cnt.ensure(nk * 4));
     HIP_TRY(w->off.ensure((nk + 1) * 4));
     HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
-    HIP_TRY(w->list.ensure(m * g.nwin * 4));
+    HIP_TRY(w->list.ensure(dh::msm_entries(g, m) * 4));
     HIP_TRY(w->buckets.ensure(2 * nk * jw * 4));
     HIP_TRY(w->segs.ensure(2 * ngroups * g.nwin * g.nseg * jw * 4));
     HIP_TRY(w->outA.ensure(ngroups * jw * 4));
     HIP_TRY(w->outB.ensure(ngroups * jw * 4));
     HIP_TRY(w->out2.ensure(2 * ngroups * jw * 4));
     HIP_TRY(w->pass.ensure(ngroups));
-    HIP_TRY(w->part.ensure(dh::msm_part_bytes(m * g.nwin, jw, 2)));
-    HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(m * g.nwin)));
+    HIP_TRY(w->part.ensure(dh::msm_part_bytes(dh::msm_entries(g, m), jw, 2)));
+    HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(dh::msm_entries(g, m))));
     dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
                   w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>(), w->part.as<uint32_t>(),
                   w->meta.as<uint32_t>(), 0};
@@ -704,7 +716,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
   HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
   HIP_TRY(w->r_scal.ensure(std::max(np, n_rounds) * 16 + 16));
-  HIP_TRY(dh::launch_scalars(d_seed, np, w->r_pstatus.as<uint8_t>(), w->r_scal.as<uint4>(), st));
+  HIP_TRY(dh::launch_scalars(d_seed, np, w->r_pstatus.as<uint8_t>(), w->r_scal.as<uint4>(), 0, st));
   HIP_TRY(hipStreamSynchronize(st));
   for (int c = 0; c < t; c++)
     if (cst[c] != 1) return fail(DH_EKEY, "public polynomial commitment %d does not decode to a subgroup point", c);
@@ -823,7 +835,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(dh::launch_prep(g2, w->r_sigbytes.as<uint8_t>(), sl, n_rounds, w->r_status2.as<uint8_t>(),
                             w->r_aff2.as<uint32_t>(), nullptr, st));
     HIP_TRY(w->r_scal.ensure(std::max(np, n_rounds) * 16 + 16));  // rounds may outnumber the partials
-    HIP_TRY(dh::launch_scalars(d_seed, n_rounds, w->r_status2.as<uint8_t>(), w->r_scal.as<uint4>(), st));
+    HIP_TRY(dh::launch_scalars(d_seed, n_rounds, w->r_status2.as<uint8_t>(), w->r_scal.as<uint4>(), 0, st));
     HIP_TRY(dh::launch_iota(w->r_entries2.as<uint32_t>(), n_rounds, st));
     // group key = commit 0 (affine, key group) — staged where the group check expects it
     HIP_TRY(w->key_aff.ensure(48 * 4));

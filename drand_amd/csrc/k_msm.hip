@@ -14,9 +14,10 @@ DH_DEV uint32_t scalar_digit(const uint4& s, int bit, int c) {
   return (uint32_t)v & ((1u << c) - 1);
 }
 
-// Signed window digits (scalars < 2^127, k_scalars): window w holds d_w = v_w + carry_w, mapped to
-// [-2^(c-1), 2^(c-1)) with a carry into the next window; the top window needs no mapping (nwin * c >= 128
-// leaves it at least one spare bit, so its digit is at most 2^(c-1)). Bucket |d| in [1, 2^(c-1)], the sign
+// Signed window digits (scalars < 2^127, or < 2^63 per half with the endomorphism split; k_scalars): window w
+// holds d_w = v_w + carry_w, mapped to
+// [-2^(c-1), 2^(c-1)) with a carry into the next window; the top window needs no mapping (nwin * c >= 128, or
+// >= 64, leaves it at least one spare bit, so its digit is at most 2^(c-1)). Bucket |d| in [1, 2^(c-1)], the sign
 // travels in bit 31 of the sorted-list entry and the bucket pass negates the point: half the buckets of
 // unsigned digits, so half the bucket-reduction work, for the same accumulation count.
 constexpr uint32_t NEG_BIT = 0x80000000u;
@@ -35,6 +36,12 @@ DH_DEV int32_t signed_digit(const uint4& s, int w, const msm_geom& g, uint32_t& 
 // grp ? grp[e] : e / gsize. The sorted list stores point indices (| NEG_BIT for a negative digit), bucket by bucket.
 DH_DEV size_t entry_group(const uint32_t* grp, size_t e, uint32_t gsize) { return grp ? grp[e] : e / gsize; }
 
+// the scalar of half h of an entry: the whole 127-bit scalar, or with the endomorphism split a = (x, y), b = (z, w)
+DH_DEV uint4 half_scalar(const uint4& s, uint32_t h, const msm_geom& g) {
+  if (g.halves == 1) return s;
+  return h ? make_uint4(s.z, s.w, 0, 0) : make_uint4(s.x, s.y, 0, 0);
+}
+
 __global__ void k_msm_hist(const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ sidx,
                            const uint32_t* __restrict__ grp, size_t m, const uint4* __restrict__ scal, msm_geom g,
                            uint32_t* __restrict__ cnt) {
@@ -42,10 +49,13 @@ __global__ void k_msm_hist(const uint32_t* __restrict__ pidx, const uint32_t* __
   if (e >= m) return;
   const uint4 s = scal[sidx ? sidx[e] : pidx[e]];
   const size_t gi = entry_group(grp, e, g.gsize);
-  uint32_t carry = 0;
-  for (int w = 0; w < g.nwin; w++) {
-    const int32_t d = signed_digit(s, w, g, carry);
-    if (d) atomicAdd(&cnt[(gi * g.nwin + w) * g.nbuck + (uint32_t)(d < 0 ? -d : d)], 1u);
+  for (uint32_t h = 0; h < g.halves; h++) {
+    const uint4 sh = half_scalar(s, h, g);
+    uint32_t carry = 0;
+    for (int w = 0; w < g.nwin; w++) {
+      const int32_t d = signed_digit(sh, w, g, carry);
+      if (d) atomicAdd(&cnt[(gi * g.nwin + w) * g.nbuck + (uint32_t)(d < 0 ? -d : d)], 1u);
+    }
   }
 }
 
@@ -54,15 +64,19 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ pidx, const uint32_t*
                               uint32_t* __restrict__ cursor, uint32_t* __restrict__ list) {
   size_t e = gtid();
   if (e >= m) return;
-  const uint32_t idx = pidx[e];
-  const uint4 s = scal[sidx ? sidx[e] : idx];
+  const uint32_t idx0 = pidx[e];
+  const uint4 s = scal[sidx ? sidx[e] : idx0];
   const size_t gi = entry_group(grp, e, g.gsize);
-  uint32_t carry = 0;
-  for (int w = 0; w < g.nwin; w++) {
-    const int32_t d = signed_digit(s, w, g, carry);
-    if (d) {
-      uint32_t pos = atomicAdd(&cursor[(gi * g.nwin + w) * g.nbuck + (uint32_t)(d < 0 ? -d : d)], 1u);
-      list[pos] = d < 0 ? (idx | NEG_BIT) : idx;
+  for (uint32_t h = 0; h < g.halves; h++) {
+    const uint4 sh = half_scalar(s, h, g);
+    const uint32_t idx = idx0 + h * g.half_stride;  // endo(P) sits half_stride points after P
+    uint32_t carry = 0;
+    for (int w = 0; w < g.nwin; w++) {
+      const int32_t d = signed_digit(sh, w, g, carry);
+      if (d) {
+        uint32_t pos = atomicAdd(&cursor[(gi * g.nwin + w) * g.nbuck + (uint32_t)(d < 0 ? -d : d)], 1u);
+        list[pos] = d < 0 ? (idx | NEG_BIT) : idx;
+      }
     }
   }
 }
@@ -370,7 +384,7 @@ static hipError_t msm_reduce(const msm_geom& g, size_t ngroups, uint32_t* bucket
 hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp, size_t m,
                            size_t ngroups, const uint4* scal, msm_ws& ws, hipStream_t st) {
   size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
-  ws.max_entries = m * (size_t)g.nwin;
+  ws.max_entries = msm_entries(g, m);
   hipError_t e = hipMemsetAsync(ws.cnt, 0, nk * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   if (m) hipLaunchKernelGGL(k_msm_hist, dim3(nblk(m, 256)), dim3(256), 0, st, pidx, sidx, grp, m, scal, g, ws.cnt);

@@ -144,7 +144,7 @@ __global__ __launch_bounds__(EXC_THREADS, 1) void k_add_iso_g2_exc(const uint32_
 // ---------------------------------------------------------------- RLC scalars
 // r_i = first 16 bytes of SHA-256(seed[32] || i_be64), 0 for rounds that failed decoding.
 __global__ __launch_bounds__(256) void k_scalars(const uint32_t* __restrict__ seed_words, size_t n,
-                                                 const uint8_t* __restrict__ status, uint4* __restrict__ scal) {
+                                                 const uint8_t* __restrict__ status, int glv, uint4* __restrict__ scal) {
   size_t i = gtid();
   if (i >= n) return;
   uint32_t w[16];
@@ -159,10 +159,32 @@ __global__ __launch_bounds__(256) void k_scalars(const uint32_t* __restrict__ se
   sha_h s = sha_iv();
   sha_compress(s, w);
   // little-endian words of a 127-bit integer (top bit cleared: the MSM's signed window digits need one spare
-  // bit; the batch check's soundness error is 2^-127 per group)
-  uint4 r = make_uint4(s.h[3], s.h[2], s.h[1], s.h[0] & 0x7fffffffu);
+  // bit; the batch check's soundness error is 2^-127 per group), or with the endomorphism split two 63-bit
+  // halves a, b: the round's scalar is a + b*mu mod r (mu = the endomorphism's eigenvalue, -z^2 on G1 or z on
+  // G2, |mu| > 2^63, so distinct (a, b) give distinct scalars: soundness error 2^-126 per group)
+  uint4 r = glv ? make_uint4(s.h[3], s.h[2] & 0x7fffffffu, s.h[1], s.h[0] & 0x7fffffffu)
+                : make_uint4(s.h[3], s.h[2], s.h[1], s.h[0] & 0x7fffffffu);
   if (status[i] != DEC_OK) r = make_uint4(0, 0, 0, 0);
   scal[i] = r;
+}
+
+// endomorphism images of the batch's points for the split MSM (G1: phi, one Fp product; G2: psi)
+template <class F>
+__global__ __launch_bounds__(256, occ<F>::W) void k_endo(size_t n, uint32_t* __restrict__ sig_aff, uint32_t* __restrict__ q_pts) {
+  size_t i = gtid();
+  if (i >= n) return;
+  aff<F> a = ld_aff_aos<F>(sig_aff, i);
+  jac<F> q = ld_jac_aos<F>(q_pts, i);
+  if constexpr (sizeof(F) == sizeof(fp)) {
+    a.x = fp_mul(a.x, fp_c(cst::BETA));
+    q.x = fp_mul(q.x, fp_c(cst::BETA));
+  } else {
+    a.x = fp2_mul(fp2_conj(a.x), fp2_c(cst::PSI_X));
+    a.y = fp2_mul(fp2_conj(a.y), fp2_c(cst::PSI_Y));
+    q = g2_psi(q);
+  }
+  st_aff_aos<F>(sig_aff, n + i, a);
+  st_jac_aos<F>(q_pts, n + i, q);
 }
 
 
@@ -195,9 +217,16 @@ hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n,
 }
 
 
-hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, hipStream_t st) {
+hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, int glv, hipStream_t st) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_scalars, dim3(nblk(n, 256)), dim3(256), 0, st, seed_words, n, status, scal);
+  hipLaunchKernelGGL(k_scalars, dim3(nblk(n, 256)), dim3(256), 0, st, seed_words, n, status, glv, scal);
+  return hipGetLastError();
+}
+
+hipError_t launch_endo(int sig_g2, size_t n, uint32_t* sig_aff, uint32_t* q_pts, hipStream_t st) {
+  if (!n) return hipSuccess;
+  if (sig_g2) hipLaunchKernelGGL(k_endo<fp2>, dim3(nblk(n, 256)), dim3(256), 0, st, n, sig_aff, q_pts);
+  else hipLaunchKernelGGL(k_endo<fp>, dim3(nblk(n, 256)), dim3(256), 0, st, n, sig_aff, q_pts);
   return hipGetLastError();
 }
 

@@ -7,9 +7,11 @@
 namespace dh {
 
 // Pippenger geometry for one MSM level: entries are cut into groups of `gsize` consecutive entries;
-// each group has nwin windows of c bits (127-bit scalars, signed digits) with nbuck = 2^(c-1) + 1 buckets
-// (index = |digit|, 0 unused);
-// bucket reduction splits the digits of a window into nseg segments of seglen digits.
+// each group has nwin windows of c bits (signed digits) with nbuck = 2^(c-1) + 1 buckets (index = |digit|,
+// 0 unused); bucket reduction splits the digits of a window into nseg segments of seglen digits.
+// Scalars: 127-bit integers (halves = 1), or with the endomorphism split (halves = 2) a pair (a, b) of 63-bit
+// integers in one uint4 (x, y = a; z, w = b): entry e then stands for two points, P_e with scalar a and
+// endo(P_e) (stored half_stride points further on) with scalar b, i.e. P_e with the scalar a + b*mu mod r.
 struct msm_geom {
   uint32_t gsize;
   int c;
@@ -17,20 +19,23 @@ struct msm_geom {
   uint32_t nbuck;
   uint32_t nseg;
   uint32_t seglen;
+  uint32_t halves;       // 1, or 2 for the endomorphism split
+  uint32_t half_stride;  // point index offset of endo(P) (halves = 2)
 };
+inline size_t msm_entries(const msm_geom& g, size_t m) { return m * (size_t)g.nwin * g.halves; }
 
 // device workspace of one MSM level (sized by the caller from msm_geom)
 struct msm_ws {
   uint32_t* cnt;       // nkeys
   uint32_t* off;       // nkeys + 1
   uint32_t* scan_tmp;  // ceil(nkeys / 4096)
-  uint32_t* list;      // m * nwin
+  uint32_t* list;      // msm_entries(g, m)
   uint32_t* buckets;   // nkeys Jacobian points (x2 for launch_msm: both point sets)
   uint32_t* segs;      // ngroups * nwin * nseg Jacobian points (x2 for launch_msm)
   uint32_t* out2;      // launch_msm: 2 * ngroups Jacobian points (sigma sums, then hash sums)
   uint32_t* part;      // balanced bucket pass: 2 Jacobian partial sums per chunk (x2 for launch_msm)
   uint32_t* meta;      // balanced bucket pass: 2 words per chunk (head kind, tail key)
-  size_t max_entries;  // set by launch_msm_sort: upper bound of sorted-list entries (m * nwin)
+  size_t max_entries;  // set by launch_msm_sort: upper bound of sorted-list entries (msm_entries)
 };
 
 // balanced bucket accumulation: entries per chunk, and workspace sizes for `max_entries` list entries
@@ -52,7 +57,11 @@ size_t hash_tmp_bytes(int sig_g2, size_t n);
 hipError_t launch_hash(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
                        const uint8_t* msgs32, size_t n, int chained, int dst_id, uint8_t* status, uint32_t* q_out, uint32_t* tmp,
                        hipStream_t st);
-hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, hipStream_t st);
+// RLC scalars from SHA-256(seed || i): 127-bit (glv = 0) or a pair of 63-bit halves (glv = 1, msm_geom.halves = 2)
+hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, int glv, hipStream_t st);
+// endomorphism images for the split MSM: sig_aff[n + i] = endo(sig_aff[i]), q_pts[n + i] = endo(q_pts[i])
+// (G1: phi(x, y) = (beta x, y); G2: psi), so the sorted lists address them as point n + i
+hipError_t launch_endo(int sig_g2, size_t n, uint32_t* sig_aff, uint32_t* q_pts, hipStream_t st);
 hipError_t launch_decode_key(int key_g2, const uint8_t* pk, uint32_t* key_aff, uint8_t* ok, hipStream_t st);
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t st);
 hipError_t launch_scan(const uint32_t* cnt, size_t nk, uint32_t* off, uint32_t* tmp, hipStream_t st);

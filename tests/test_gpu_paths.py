@@ -462,3 +462,57 @@ def test_hash_to_curve_rfc9380_device(dh):
         sig = s.sign_beacons(one, rounds)
         gen = dh.hash_to_curve(group, [s.digest_beacon(int(r)) for r in rounds], dst)
         assert [x.tobytes() for x in sig] == gen, name
+
+
+# ---------------------------------------------------------------- the batch check itself, not only the verdicts
+@pytest.mark.parametrize("scheme", ["bls-unchained-g1-rfc9380", "bls-unchained-on-g1", "pedersen-bls-unchained",
+                                    CHAINED])
+def test_group_checks_pass_on_clean_batches(dh, scheme):
+    """Verdicts alone cannot show a broken MSM: bisection down to per-round leaves still gets every verdict right.
+    So the batch statistics are checked: a clean batch (with one undecodable round, scalar 0) passes its single
+    level-0 group check, and a batch with one forged round fails exactly one group per bisection level and sends
+    at most a handful of rounds to leaves. This pins the random-linear-combination sums, including the
+    endomorphism split (scalars a + b*mu with endo(P) images, k_endo) at every level."""
+    import ctypes
+    import torch
+    from drand_amd import _lib
+    lib = _lib.load()
+    s = dh.scheme_from_name(scheme)
+    sk = _secret(b"clean-" + scheme.encode())
+    n = 6000 if s.sig_len == 48 else 3000
+    rounds = np.arange(1, n + 1, dtype=np.uint64)
+    prevs = None
+    if s.chained:
+        rng = np.random.default_rng(11)
+        prevs = rng.integers(0, 256, (n, 96), dtype=np.uint8)
+        sigs = s.sign_beacons(sk, rounds, [p.tobytes() for p in prevs])
+    else:
+        sigs = s.sign_beacons(sk, rounds)
+    pk = s.public_key(sk)
+    sigs[77, 9] ^= 0x01  # off the curve (or at least not this round's point): rejected, its scalar never counts
+    dev = torch.device("cuda", 0)
+    d_r = torch.from_numpy(rounds.view(np.int64)).to(dev)
+    d_p = torch.from_numpy(np.ascontiguousarray(prevs)).to(dev) if prevs is not None else None
+
+    def run(sg, seed):
+        d_s = torch.from_numpy(sg).to(dev)
+        d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+        stats = (ctypes.c_uint64 * 4)()
+        rc = lib.dh_verify_batch_device(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr()), ctypes.c_void_p(d_s.data_ptr()),
+                                        s.sig_len, ctypes.c_void_p(d_p.data_ptr()) if d_p is not None else None,
+                                        96 if d_p is not None else 0, None, n, ctypes.c_void_p(d_v.data_ptr()), None,
+                                        seed, None, stats)
+        assert rc == 0, _lib.last_error()
+        torch.cuda.synchronize()
+        return d_v.cpu().numpy(), list(stats)
+
+    v, st = run(sigs, 5)
+    assert np.flatnonzero(v == 0).tolist() == [77], st  # rejected at decode (off the curve or off the subgroup)
+    assert st[:3] == [1, 0, 0], st  # one level, no failed group, no leaf
+    forged = sigs.copy()
+    k = 4321 % n
+    forged[k] = forged[k + 1]  # a valid point of another round
+    v2, st2 = run(forged, 6)
+    assert sorted(np.flatnonzero(v2 == 0).tolist()) == sorted({77, k}), st2
+    assert st2[0] >= 2 and st2[1] == st2[0], st2  # exactly one failing group per level: the forged round's
+    assert 1 <= st2[2] <= 16, st2  # leaves: the rounds of its last group only
