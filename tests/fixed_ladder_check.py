@@ -1,6 +1,7 @@
 """Child process for tests/test_gpu_parity.py::test_fixed_bisection_ladder: with DRANDHIP_BISECT set by the parent
 (a fixed ladder of group sizes instead of the expected-cost choice), verifies a quicknet batch with 0.5% corrupted
-rounds and prints the rejected indices and the expected set as JSON."""
+rounds, then a G2 (pedersen-bls-unchained) batch with one forged round through the device entry point, and prints
+the rejected indices, the expected sets and the G2 batch statistics as JSON."""
 import hashlib
 import json
 import os
@@ -24,4 +25,28 @@ for k, i in enumerate(bad):
     else:
         sigs[i, 0] ^= 0x20
 v, _ = s.verify_beacons(pk, rounds, sigs, seed=21)
-print(json.dumps({"rejected": np.flatnonzero(~v).tolist(), "expected": bad.tolist()}))
+out = {"rejected": np.flatnonzero(~v).tolist(), "expected": bad.tolist()}
+
+# G2: one forged round; every bisection level of the ladder must fail exactly one group (its group)
+import ctypes  # noqa: E402
+import torch  # noqa: E402
+from drand_amd import _lib  # noqa: E402
+torch.zeros(1, device="cuda")
+lib = _lib.load()
+g2 = scheme_from_name("pedersen-bls-unchained")
+m = 3000
+r2 = np.arange(1, m + 1, dtype=np.uint64)
+s2 = g2.sign_beacons(sk, r2)
+s2[1234] = s2[1235]
+pk2 = g2.public_key(sk)
+dev = torch.device("cuda", 0)
+d_r, d_s = torch.from_numpy(r2.view(np.int64)).to(dev), torch.from_numpy(s2).to(dev)
+d_v = torch.zeros(m, dtype=torch.uint8, device=dev)
+stats = (ctypes.c_uint64 * 4)()
+rc = lib.dh_verify_batch_device(g2.id, pk2, len(pk2), ctypes.c_void_p(d_r.data_ptr()), ctypes.c_void_p(d_s.data_ptr()),
+                                g2.sig_len, None, 0, None, m, ctypes.c_void_p(d_v.data_ptr()), None, 7, None, stats)
+assert rc == 0, _lib.last_error()
+torch.cuda.synchronize()
+out["g2_rejected"] = np.flatnonzero(d_v.cpu().numpy() == 0).tolist()
+out["g2_stats"] = list(stats)
+print(json.dumps(out))

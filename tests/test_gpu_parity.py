@@ -343,6 +343,11 @@ def test_fixed_bisection_ladder(dh, ladder):
     assert r.returncode == 0, r.stderr[-2000:]
     got = json.loads(r.stdout.strip().splitlines()[-1])
     assert got["rejected"] == got["expected"] and len(got["expected"]) == 200
+    # G2 with one forged round: every level of the ladder fails exactly its group, leaves = the last size
+    levels, failed, leaves, rejected = got["g2_stats"]
+    last = int(ladder.split(",")[-1])
+    assert got["g2_rejected"] == [1234] and rejected == 1
+    assert levels >= 2 and failed == levels and leaves == last, got["g2_stats"]
 
 
 def test_device_entry_stats(dh):

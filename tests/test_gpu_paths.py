@@ -515,5 +515,7 @@ def test_group_checks_pass_on_clean_batches(dh, scheme):
     v2, st2 = run(forged, 6)
     assert sorted(np.flatnonzero(v2 == 0).tolist()) == sorted({77, k}), st2
     # exactly one failing group per level (the forged round's): every other group's sums check out at every level
-    assert st2[0] >= 2 and st2[1] == st2[0], st2
-    assert 1 <= st2[2] <= 1024, st2  # leaves: the rounds of its last failing group only (the cost model's size)
+    # (the cost model may also go from the failed level 0 straight to leaves; tests/fixed_ladder_check.py forces
+    # bisection levels on G1 and G2)
+    assert st2[1] == st2[0], st2
+    assert 1 <= st2[2] <= (n if st2[0] == 1 else 1024), st2
