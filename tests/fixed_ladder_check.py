@@ -9,8 +9,13 @@ import sys
 
 import numpy as np
 
+import torch  # noqa: E402
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from drand_amd import scheme_from_name  # noqa: E402
+
+# torch carries its own HIP runtime: bring it up before the library's runtime has created its streams
+torch.zeros(1, device="cuda")
 
 s = scheme_from_name("bls-unchained-g1-rfc9380")
 sk = hashlib.sha256(b"ladder").digest()
@@ -29,9 +34,7 @@ out = {"rejected": np.flatnonzero(~v).tolist(), "expected": bad.tolist()}
 
 # G2: one forged round; every bisection level of the ladder must fail exactly one group (its group)
 import ctypes  # noqa: E402
-import torch  # noqa: E402
 from drand_amd import _lib  # noqa: E402
-torch.zeros(1, device="cuda")
 lib = _lib.load()
 g2 = scheme_from_name("pedersen-bls-unchained")
 m = 3000
