@@ -85,6 +85,10 @@ struct dbuf {
 
 struct worker {
   hipStream_t stream = nullptr;
+  // high-priority stream for a batch's latency-bound tail (MSM, pairing checks, bisection): its small kernels
+  // get wave slots ahead of other batches' saturating per-round kernels (verify_core)
+  hipStream_t tail = nullptr;
+  hipEvent_t handoff = nullptr;
   bool busy = false;
   // per-round state
   dbuf status, sig_aff, q_pts, scal, entries, verdict_tmp, rand_tmp, h2c_tmp;
@@ -117,7 +121,10 @@ struct worker {
                    &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
-    stream = nullptr;
+    if (tail) (void)hipStreamDestroy(tail);
+    if (handoff) (void)hipEventDestroy(handoff);
+    stream = tail = nullptr;
+    handoff = nullptr;
   }
 };
 
@@ -185,6 +192,12 @@ struct lease {
 int set_device_and_stream(worker* w) {
   HIP_TRY(hipSetDevice(g_ctx.device));
   if (!w->stream) HIP_TRY(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+  if (!w->tail) {
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&w->tail, hipStreamNonBlocking, greatest));
+  }
+  if (!w->handoff) HIP_TRY(hipEventCreateWithFlags(&w->handoff, hipEventDisableTiming));
   return DH_OK;
 }
 
@@ -553,6 +566,15 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     }
     if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
     HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
+  }
+  // the tail (MSM, checks, bisection) runs on the worker's high-priority stream, after the per-round kernels
+  if (w->tail && st == w->stream) {
+    if (mode <= VM_BEGIN) {
+      HIP_TRY(hipEventRecord(w->handoff, st));
+      HIP_TRY(hipStreamWaitEvent(w->tail, w->handoff, 0));
+    }
+    st = w->tail;
+    T.st = st;
   }
 
   // bisection levels: group sizes n, then next_group_size() per level, then per-round leaves (a failing group is re-checked
