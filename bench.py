@@ -50,7 +50,8 @@ def parse():
                     help="leave the library's HIP-event stage timing off inside the timed region")
     ap.add_argument("--roofline-steps", type=int, default=2, help="single-stream batches timed for the roofline")
     ap.add_argument("--single-call-steps", type=int, default=4, help="one-call-at-a-time batches timed after")
-    ap.add_argument("--single-call-split", default="262144,3", help="chunk rounds,workers of the one-call split")
+    ap.add_argument("--single-call-split", default="0,1", help="chunk rounds,workers of the one-call split (library "
+                    "default: none)")
     ap.add_argument("--streams", type=int, default=8,
                     help="batches in flight per GPU (host threads, each with its own HIP stream in libdrandhip)")
     ap.add_argument("--split", default="0",
@@ -247,7 +248,7 @@ def main():
         dt = time.perf_counter() - t1
         single = {"value": round(n * args.single_call_steps / dt, 1), "unit": "beacons/s",
                   "ms_per_call": round(dt * 1000 / args.single_call_steps, 3),
-                  "split": "%d-round chunks x %d streams, per-round kernels chained across them" % (chunk, workers),
+                  "split": ("%d-round chunks x %d streams" % (chunk, workers)) if chunk else "none (library default)",
                   "calls": args.single_call_steps}
         # the CheckPastBeacons shape: one call over a whole stored chain (4 x the bench window, the same signed
         # rounds repeated); the call's one exposed tail is amortised over 4x the rounds

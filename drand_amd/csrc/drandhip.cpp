@@ -904,18 +904,18 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   return DH_OK;
 }
 
-// ---- one call over many internal streams (the drop-in callers make ONE call per window)
-// A batch of n rounds is cut into chunks verified by up to `workers` leased workers (each its own HIP stream and
-// workspace). The chunks' per-round kernels are chained in chunk order across the streams (prep_gate), so each
-// runs alone at the chip's full rate, while earlier chunks' MSMs and latency-bound group checks run beside them:
-// the call costs about the sum of the per-round kernels plus ONE chunk's tail. Streams map onto the process's
-// hardware queues (GPU_MAX_HW_QUEUES, 4 by default, one of them usually held by the caller's own stream), and two
-// streams on one queue run in order, so a tail would block the next chunk's kernels: 3 workers by default. Every
-// chunk is a complete batch check (its own RLC scalars: seed + chunk index when the caller fixed a seed, fresh
-// CSPRNG seeds otherwise), so verdicts stay bit-exact per round. DRANDHIP_SPLIT="chunk,workers" overrides the
-// defaults (262144 rounds, 3 workers); "0" disables splitting.
+// ---- one call over several internal streams (the drop-in callers make ONE call per window)
+// Off by default: measured on the MI355X (profiles/split_sweep_r02k_*.jsonl), one stream per call is the fastest
+// form of a call (1M rounds 64.9 ms, 4M 225.8 ms = 92% of the 8-batches-in-flight rate) — a chunk's per-round
+// kernels alone on the chip are no faster than one large launch, and the chunks' latency-bound tails, made of
+// many small kernels, wait for wave slots the per-round kernels hold and slow them. When enabled
+// (DRANDHIP_SPLIT="chunk,workers" or dh_set_split), a batch is cut into chunks, each a complete batch check (its own
+// RLC scalars: seed + chunk index when the caller fixed a seed, fresh CSPRNG seeds otherwise, so verdicts stay
+// bit-exact per round), verified by up to `workers` leased workers; the chunks' per-round kernels are chained in
+// chunk order across the workers' streams (prep_gate) and each chunk's tail runs on its worker's high-priority
+// stream. Streams share the process's hardware queues (GPU_MAX_HW_QUEUES, 4 by default per priority).
 struct split_cfg {
-  size_t chunk = 262144;
+  size_t chunk = 0;  // 0: one stream per call
   int workers = 3;
 };
 std::mutex g_split_mu;

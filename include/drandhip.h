@@ -74,18 +74,18 @@ int dh_key_len(int scheme);
  *   verdict_out  n bytes: 1 = VerifyBeacon returns nil, 0 = it returns an error
  *   rand_out     n*32 bytes SHA-256(sig) (RandomnessFromSignature) or NULL
  *   seed         0 = draw the random-linear-combination seed from the OS CSPRNG; otherwise deterministic
- * One call uses several internal HIP streams for large n: the rounds are cut into chunks (262 144 rounds by
- * default), each a complete batch check, verified by up to 3 workers; the chunks' per-round kernels run one
- * after another at the chip's full rate while earlier chunks' MSMs and group checks run beside them, so a call
- * costs about its per-round work plus one chunk's latency tail. DRANDHIP_SPLIT="chunk,workers" changes this
- * ("0": one stream per call).
+ * One call runs on one internal stream by default (its per-round kernels, then its MSM and pairing checks on a
+ * high-priority stream): a 4M-round call runs at 92% of the rate of 8 concurrent 1M calls, a 1M-round call at
+ * 81% (its ~16 ms latency tail is exposed). DRANDHIP_SPLIT="chunk,workers" / dh_set_split cut a call into
+ * chunks verified on several streams instead.
  * Returns DH_OK or a negative error code (no verdicts are valid on error).
  */
 int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* rounds, const uint8_t* sigs,
                     size_t sig_stride, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens, size_t n,
                     uint8_t* verdict_out, uint8_t* rand_out, uint64_t seed);
 
-/* Set the one-call split of dh_verify_batch / dh_verify_batch_device (chunk_rounds 0 = one stream per call). */
+/* Set the one-call split of dh_verify_batch / dh_verify_batch_device (chunk_rounds 0 = one stream per call, the
+ * default). */
 int dh_set_split(uint64_t chunk_rounds, int workers);
 
 /*
