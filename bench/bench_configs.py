@@ -163,9 +163,16 @@ def cfg_chained(args):
     bad = chainsynth.corrupted_rounds(n, n_bad)
     rng = np.random.default_rng(0xC5)
     t0 = time.perf_counter()
-    sigs = chainsynth.sign_chain(s, sk, 1, n, genesis, bad, rng,
-                                 progress=lambda p, m: print("chain: step %d / %d (%.0f s)" % (p, m, time.perf_counter() - t0),
-                                                             file=sys.stderr, flush=True))
+    cache = os.path.join(args.chain_cache, "chain_%d_%d.npy" % (n, n_bad)) if args.chain_cache else None
+    if cache and os.path.exists(cache):  # the same seeded chain, signed by an earlier run (ladder sweeps)
+        sigs = np.load(cache)
+    else:
+        sigs = chainsynth.sign_chain(s, sk, 1, n, genesis, bad, rng,
+                                     progress=lambda p, m: print("chain: step %d / %d (%.0f s)" % (
+                                         p, m, time.perf_counter() - t0), file=sys.stderr, flush=True))
+        if cache:
+            os.makedirs(args.chain_cache, exist_ok=True)
+            np.save(cache, sigs)
     t_sign = time.perf_counter() - t0
     import random
     chainsynth.corrupt(sigs, bad, random.Random(31))
@@ -318,6 +325,7 @@ def main():
     ap.add_argument("--subsets", choices=["first", "random"], default="first")
     ap.add_argument("--cpu-sample", type=int, default=2000)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--chain-cache", default=None, help="directory for the signed chained chain (reused by later runs)")
     ap.add_argument("--split", default="0", help="the library's one-call split (DRANDHIP_SPLIT): off, so each of the "
                     "--streams batches in flight is one stream")
     args = ap.parse_args()

@@ -1,20 +1,24 @@
 #!/bin/bash
-# Bisection-ladder sweep over 1M corrupted rounds (chained replay by default; quicknet / unchained), one stream:
-#   bash bench/bisect_sweep.sh <tag> [chained|quicknet|unchained]
-# adaptive (default) vs the fixed r01 ladder at three fault densities set through DRANDHIP_BISECT; one JSON line per ladder.
+# Bisection-ladder sweep on the chained-replay config (a real sequential chain, Cfg5 corruption classes), one
+# stream, one 1M window: the adaptive ladder (next_group_size) against fixed ladders set through DRANDHIP_BISECT
+# (read when the library loads, so one process per ladder; the chain is signed once and cached).
+#   bash bench/bisect_sweep.sh <tag> [rounds] [densities] [ladders]
 set -euo pipefail
 TAG=${1:-dev}
+N=${2:-1048576}
+DENS=${3:-"0.001 0.0001"}
+LADDERS=${4:-"adaptive 256,16,2 128,8 64,4 512,32,4 32"}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
 mkdir -p "$O"
 cd "$R"
-CFG=${2:-chained}
-ARGS="$CFG --streams 1 --steps 2 --warmup 1 --cpu-sample 100 --cpu-threads 4"
-for C in 0.001 0.000001 0.01; do
-  for L in adaptive 4096,256,16,2; do
+for C in $DENS; do
+  for L in $LADDERS; do
     if [ "$L" = adaptive ]; then unset DRANDHIP_BISECT; else export DRANDHIP_BISECT=$L; fi
     echo "corrupt $C ladder $L" >> "$O/bisect_$TAG.txt"
-    timeout -k 10 150 python bench/bench_configs.py $ARGS --corrupt $C >> "$O/bisect_$TAG.txt" 2>> "$O/bisect_$TAG.err"
+    timeout -k 10 300 python bench/bench_configs.py chained --rounds $N --window $N --streams 1 --steps 2 \
+      --cpu-sample 10 --cpu-threads 4 --corrupt $C --chain-cache "$O/chain_cache" >> "$O/bisect_$TAG.txt" 2>> "$O/bisect_$TAG.err"
   done
 done
+rm -rf "$O/chain_cache"
 echo "sweep $TAG done"
