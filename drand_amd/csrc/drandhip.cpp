@@ -394,13 +394,15 @@ static bool lane_pairing() {
   return v;
 }
 
+// key_h: [h_eff] pk next to a decoded G2 key (k_decode_key), or null (the check clears B's cofactor itself)
 static hipError_t group_check(worker* w, bool g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key,
-                              uint8_t* pass, hipStream_t st) {
+                              uint8_t* pass, hipStream_t st, const uint32_t* key_h = nullptr) {
   if (lane_pairing()) return dh::launch_group_check(g2, A, B, ngroups, key, pass, st);
   hipError_t e;
   if ((e = w->vm_pairs.ensure(ngroups * 2 * 72 * 4)) != hipSuccess) return e;
   if ((e = w->vm_live.ensure(ngroups * 2)) != hipSuccess) return e;
-  return dh::launch_group_check_vm(g2, A, B, ngroups, key, w->vm_pairs.as<uint32_t>(), w->vm_live.as<uint8_t>(), pass, st);
+  return dh::launch_group_check_vm(g2, A, B, ngroups, key, g2 ? nullptr : key_h, w->vm_pairs.as<uint32_t>(),
+                                   w->vm_live.as<uint8_t>(), pass, st);
 }
 
 static hipError_t leaf_check(worker* w, bool g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff,
@@ -513,7 +515,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (mode <= VM_BEGIN) {
     // key
     HIP_TRY(w->key_raw.ensure(96));
-    HIP_TRY(w->key_aff.ensure(48 * 4));  // key-group affine point (G2: 48 words); fixed size keeps the key cache valid
+    // key-group affine point (G2: 48 words) + [h_eff] pk (48 words, G1 schemes); fixed size keeps the key cache valid
+    HIP_TRY(w->key_aff.ensure(96 * 4));
     HIP_TRY(w->key_ok.ensure(64));  // [0] key status, [32..63] RLC seed
     uint8_t key_ok = 0;
     const bool key_hit = w->cached_key_len == pk_len && w->cached_key_g2 == (g2 ? 0 : 1) && !memcmp(w->cached_key, pk, pk_len);
@@ -624,7 +627,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     } else {
       HIP_TRY(T.run(chk_names[std::min(level, 7)], [&] {
         return group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups, w->key_aff.as<uint32_t>(),
-                           w->pass.as<uint8_t>(), st);
+                           w->pass.as<uint8_t>(), st, w->key_aff.as<uint32_t>() + 48);
       }));
     }
     HIP_TRY(dh::launch_mark_groups(w->entries.as<uint32_t>(), m, gsize, w->pass.as<uint8_t>(), w->status.as<uint8_t>(),
@@ -860,7 +863,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(dh::launch_scalars(d_seed, n_rounds, w->r_status2.as<uint8_t>(), w->r_scal.as<uint4>(), 0, st));
     HIP_TRY(dh::launch_iota(w->r_entries2.as<uint32_t>(), n_rounds, st));
     // group key = commit 0 (affine, key group) — staged where the group check expects it
-    HIP_TRY(w->key_aff.ensure(48 * 4));
+    HIP_TRY(w->key_aff.ensure(96 * 4));
     HIP_TRY(hipMemcpyAsync(w->key_aff.p, w->r_caff.p, kaw * 4, hipMemcpyDeviceToDevice, st));
     w->cached_key_len = 0;  // key_aff now holds this call's key
     const dh::msm_geom g = geom_for(n_rounds);
@@ -1225,7 +1228,7 @@ int dh_check_partials(int scheme, const uint8_t* pk, size_t pk_len, const uint8_
   if (rc) return rc;
   hipStream_t st = w->stream;
   HIP_TRY(w->key_raw.ensure(96));
-  HIP_TRY(w->key_aff.ensure(48 * 4));
+  HIP_TRY(w->key_aff.ensure(96 * 4));  // key + [h_eff] key (k_decode_key)
   HIP_TRY(w->key_ok.ensure(64));
   HIP_TRY(w->outA.ensure(jw * 4));
   HIP_TRY(w->outB.ensure(jw * 4));
@@ -1234,7 +1237,8 @@ int dh_check_partials(int scheme, const uint8_t* pk, size_t pk_len, const uint8_
   HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(), w->key_ok.as<uint8_t>(), st));
   w->cached_key_len = 0;  // key_aff is rewritten here: the batch path re-decodes its key on this worker
   HIP_TRY(dh::launch_sum_partials(g2, (const uint32_t*)d_partials, k, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st));
-  HIP_TRY(group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), 1, w->key_aff.as<uint32_t>(), w->pass.as<uint8_t>(), st));
+  HIP_TRY(group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), 1, w->key_aff.as<uint32_t>(), w->pass.as<uint8_t>(), st,
+                      w->key_aff.as<uint32_t>() + 48));
   uint8_t key_ok = 0, pass = 0;
   HIP_TRY(hipMemcpyAsync(&key_ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(&pass, w->pass.p, 1, hipMemcpyDeviceToHost, st));

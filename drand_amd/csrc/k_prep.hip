@@ -202,6 +202,13 @@ __global__ void k_decode_key(const uint8_t* __restrict__ pk, uint32_t* __restric
     a.y = K{};
   }
   st_aff_aos<K>(key_aff, 0, a);
+  if constexpr (sizeof(K) == sizeof(fp2)) {
+    // G1-signature schemes: also [h_eff] pk (h_eff = 1 - z = |z| + 1), so the batch check can read
+    // e([h_eff] B, pk) as e(B, [h_eff] pk) and skip the per-check cofactor clearing (k_vm_prep_groups)
+    aff<fp2> h = a;
+    if (st == DEC_OK) h = jac_to_aff(jac_add(jac_mul_uabs(a), jac_from_aff(a)));
+    st_aff_aos<fp2>(key_aff, 1, h);
+  }
 }
 
 

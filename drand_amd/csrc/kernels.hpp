@@ -82,7 +82,9 @@ hipError_t launch_leaf_check(int sig_g2, const uint32_t* entries, size_t m, cons
                              const uint32_t* key_aff, const uint8_t* status, uint8_t* verdict, hipStream_t st);
 
 // lane-parallel pairing checks (k_vm.hip): pairs = 2 x 72 words per check, live = 2 bytes, done = 1 byte
+// key_h: [h_eff] pk for G1-signature schemes (k_decode_key writes it after the key), or null for [h_eff] B
 hipError_t launch_group_check_vm(int sig_g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_aff,
+                                 const uint32_t* key_h,
                                  uint32_t* pairs, uint8_t* live, uint8_t* pass, hipStream_t st);
 hipError_t launch_leaf_check_vm(int sig_g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
                                 const uint32_t* key_aff, const uint8_t* status, uint32_t* pairs, uint8_t* live, uint8_t* done,

@@ -94,3 +94,19 @@ def test_hash_to_curve_rfc9380_vectors(oracle):
         assert (px0, px1, py0) == (int(x0, 16), int(x1, 16), int(y0, 16)), msg
         if y1 is not None:
             assert py1 == int(y1, 16)
+
+
+def test_cofactor_moves_to_the_key_side():
+    """The G1-signature batch check reads e([h_eff] B, pk) as e(B, [h_eff] pk) with B = sum r_i Q_i the unreduced
+    RLC sum of hash points (NOT in G1; k_vm.hip k_vm_prep_groups). Pinned here with the oracle's generic pairing on
+    a point of E1(Fp) off the subgroup, with a negative control."""
+    import random
+    import bls_py as B
+    rng = random.Random(7)
+    Q = B.iso_map_g1(B.sswu_g1(rng.randrange(B.P)))
+    assert B.ec_mul(B.FP, Q, B.R) is not None  # off G1
+    pk = B.ec_mul(B.FP2, B.G2_GEN, rng.randrange(1, B.R))
+    h = B.H_EFF_G1
+    hQ, hpk, negQ = B.ec_mul(B.FP, Q, h), B.ec_mul(B.FP2, pk, h), B.ec_neg(B.FP, Q)
+    assert B.pairing_check([(hQ, pk), (negQ, hpk)])
+    assert not B.pairing_check([(hQ, pk), (negQ, pk)])
