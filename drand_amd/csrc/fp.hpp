@@ -12,6 +12,7 @@
 #include <stdint.h>
 #include "consts.hpp"
 #include "fp_mul_fips.hpp"
+#include "fp_mul28.hpp"
 
 namespace dh {
 
@@ -166,7 +167,9 @@ DH_DEV fp fp_mul_cios(const fp& a, const fp& b) {
   return r;
 }
 
-// The field product used everywhere: product-scanning Montgomery (fp_mul_fips.hpp), one out-of-line copy
+// The field product used everywhere: product-scanning Montgomery on 14 x 28-bit limbs behind the 12 x 32-bit
+// interface (fp_mul28.hpp: one v_mad_u64_u32 per partial product, no carry adds; the 32-bit form of
+// fp_mul_fips.hpp needs a v_addc per product and measured 17% slower), one out-of-line copy
 // per code object so that the large kernels (pairing, hash-to-curve) stay compact; define DH_MUL_INLINE to
 // inline it instead.
 //
@@ -175,8 +178,7 @@ DH_DEV fp fp_mul_cios(const fp& a, const fp& b) {
 // only ~108 VGPRs can carry values across a product — 4 Fp2 elements. The G2 point formulas keep more
 // than that live and spilled to scratch around EVERY product (k_prep_msg<fp2>: 19.3 KB of scratch per
 // lane). The products are therefore entered through an inline-asm `s_swappc_b64` whose clobber list is
-// exactly what the two bodies touch: v0-v39, v48, s0-s15, s30-s31, vcc and scc (the squaring also v49-55,
-// v64-71, v80-81). The bodies are ordinary compiled functions: they may set SCC and mask EXEC around a
+// exactly what the two bodies touch: v0-v39, v48-v53, s0-s17, s30-s31, vcc and scc. The bodies are ordinary compiled functions: they may set SCC and mask EXEC around a
 // branch (restoring it), so SCC must be in the list — without it a loop condition held in SCC across a
 // product was lost. Everything else stays live in registers across the call. drand_amd/tools/check_fp_abi.py
 // disassembles every built code object and fails the build if a body touches a register outside that list,
@@ -187,7 +189,7 @@ extern "C" __device__ __noinline__ __attribute__((used)) fpvec dh_fp_mul_vec(fpv
   uint32_t x[12], y[12], r[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) { x[i] = a[i]; y[i] = b[i]; }
-  fips_mont_mul(r, x, y);
+  m28::mul(r, x, y);
   fpvec o;
 #pragma unroll
   for (int i = 0; i < 12; i++) o[i] = r[i];
@@ -197,7 +199,7 @@ extern "C" __device__ __noinline__ __attribute__((used)) fpvec dh_fp_sqr_vec(fpv
   uint32_t x[12], r[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) x[i] = a[i];
-  fips_mont_sqr(r, x);
+  m28::sqr(r, x);
   fpvec o;
 #pragma unroll
   for (int i = 0; i < 12; i++) o[i] = r[i];
@@ -206,12 +208,8 @@ extern "C" __device__ __noinline__ __attribute__((used)) fpvec dh_fp_sqr_vec(fpv
 
 #define DH_FP_CALL_CLOBBERS                                                                                    \
   "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", \
-      "v48", "s0", "s1", "s2", "s3", "s4", "s5", "s6", "s7", "s8", "s9", "s10", "s11", "s12", "s13", "s14", "s15",  \
-      "s30", "s31", "vcc", "scc"
-// the squaring's body also works in the caller-saved stripes v49-v55, v64-v71, v80-v81
-#define DH_FP_SQR_EXTRA_CLOBBERS                                                                                  \
-  "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v80", \
-      "v81"
+      "v48", "v49", "v50", "v51", "v52", "v53", "s0", "s1", "s2", "s3", "s4", "s5", "s6", "s7", "s8", "s9", "s10",  \
+      "s11", "s12", "s13", "s14", "s15", "s16", "s17", "s30", "s31", "vcc", "scc"
 // a = a * b (a in v0-v11, b in v12-v23 and clobbered); the callee address is formed exactly as the compiler
 // forms it for a direct call
 #define DH_FP_CALL(fn) \
@@ -252,8 +250,7 @@ DH_DEV fp fp_sqr(const fp& a) {
   asm(DH_FP_CALL("dh_fp_sqr_vec")
       : "+{v[0:11]}"(x)
       :
-      : "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", DH_FP_CALL_CLOBBERS,
-        DH_FP_SQR_EXTRA_CLOBBERS);
+      : "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", DH_FP_CALL_CLOBBERS);
   return from_vec(x);
 #endif
 }

@@ -1,8 +1,7 @@
 // Fp Montgomery product and squaring on 14 x 28-bit limbs behind the 12 x 32-bit interface of fp.hpp.
-// NOT wired into the library yet: as out-of-line bodies (dh_fp_mul_vec / dh_fp_sqr_vec) they touch v49-v53 and
-// s16-s17 beyond today's declared call clobbers, so switching to them means widening DH_FP_CALL_CLOBBERS together
-// with the allowed sets of drand_amd/tools/check_fp_abi.py — a change to that build-time guard, left for review.
-// Today the header is exercised by bench/microbench_fp28.hip only.
+// These are the bodies of the library's out-of-line field products (fp.hpp dh_fp_mul_vec / dh_fp_sqr_vec; call
+// clobbers v0-v39, v48-v53, s0-s17, checked at build time by drand_amd/tools/check_fp_abi.py) and of the pairing
+// VM's inlined products (k_vm.hip); bench/microbench_fp28.hip measures them against the 32-bit form.
 //
 // Why 28 bits: on gfx950 the 32-bit product-scanning step is a v_mad_u64_u32 PLUS a v_addc_co_u32 for the carry
 // into the column's third word, and the carry add issues as slowly as the multiply (~19 T MAC/s either way against

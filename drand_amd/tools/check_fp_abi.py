@@ -4,8 +4,8 @@
 The kernels enter dh_fp_mul_vec / dh_fp_sqr_vec through an inline-asm s_swappc_b64 whose clobber list
 names exactly the registers the two bodies may touch. The bodies are ordinary compiled functions, so this
 script disassembles every gfx950 code object it is given and fails (exit 1) if a body
-  * mentions a VGPR outside its declared set (v0-v39, v48; the squaring also v49-55, v64-71, v80-81) or an
-    SGPR outside s0-s15, s30-s31 (plus vcc / exec reads),
+  * mentions a VGPR outside its declared set (v0-v39, v48-v53) or an SGPR outside s0-s17, s30-s31 (plus vcc /
+    exec reads), ranged operands (v[4:5]) included,
   * touches the stack (scratch_* / buffer_* instructions, s32 / s33), or calls anything,
   * writes s[30:31] (the return address) or does not return with s_setpc_b64 s[30:31],
   * writes M0, or writes EXEC other than restoring it after an s_and_saveexec (SCC and VCC are clobbered).
@@ -20,10 +20,12 @@ import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 FUNCS = ("dh_fp_mul_vec", "dh_fp_sqr_vec")
-ALLOWED_V = {"dh_fp_mul_vec": set(range(0, 40)) | {48},  # fp.hpp DH_FP_CALL_CLOBBERS (+ the v0-v23 operands)
-             "dh_fp_sqr_vec": set(range(0, 40)) | set(range(48, 56)) | set(range(64, 72)) | {80, 81}}  # + SQR_EXTRA
-ALLOWED_S = set(range(0, 16)) | {30, 31}
-REG = re.compile(r"\b([vs])(?:\[(\d+):(\d+)\]|(\d+))\b")
+# fp.hpp DH_FP_CALL_CLOBBERS (+ the v0-v23 operands); the 28-bit bodies (fp_mul28.hpp) need no extra stripes
+ALLOWED_V = {"dh_fp_mul_vec": set(range(0, 40)) | set(range(48, 54)),
+             "dh_fp_sqr_vec": set(range(0, 40)) | set(range(48, 54))}
+ALLOWED_S = set(range(0, 18)) | {30, 31}
+# ranged operands (v[4:5]) end in "]", after which \b never matches: only the single-register form takes \b
+REG = re.compile(r"\b([vs])(?:\[(\d+):(\d+)\]|(\d+)\b)")
 
 
 def device_elf(obj, tmp):
