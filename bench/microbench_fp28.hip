@@ -1,10 +1,11 @@
-// Microbenchmark: a 14 x 28-bit-limb Montgomery product for Fp against the 12 x 32-bit product of fp.hpp.
-// With 28-bit limbs a 28x28 product is < 2^56, so a 64-bit column accumulator absorbs every product of a column
-// (<= 28 of them plus the carry-in) with ONE v_mad_u64_u32 each and no carry add; the 32-bit form needs a
-// v_addc_co_u32 per product, which costs as much as the multiply (profiles/microbench_carry_r02.txt).
-// The 12 x 32-bit interface is kept: x is sliced into 28-bit limbs, y into 28-bit limbs of y * 2^8, so the
-// 28-bit Montgomery product (R = 2^392) returns x * y * 2^8 / 2^392 = x * y / 2^384, the same value as fp_mul.
-// Checks every result against dh::fp_mul / dh::fp_sqr and reports mismatches.
+// Microbenchmark: Fp Montgomery products on gfx950 in the forms the library has used, at controlled occupancy.
+//   mul32 / sqr32        12 x 32-bit product scanning, inlined (fp_mul_fips.hpp: a v_addc per partial product)
+//   mul28 / sqr28        14 x 28-bit limbs, one 64-bit column accumulator chain (fp_mul28.hpp m28::mul / sqr)
+//   mul28i / sqr28i      the same with each column's off-critical-path terms in two independent accumulators
+//                        (m28::mul_ilp / sqr_ilp)
+//   call                 the library's out-of-line product (fp.hpp dh::fp_mul / fp_sqr through DH_FP_CALL)
+// Each lane runs ONE dependent chain x = x * y (or x = x^2), as a pairing program or an exponentiation does, at 1, 2
+// and 8 waves per SIMD (blocks of 256 threads = 1 wave per SIMD per CU). Every form's result is compared with mul32.
 // Build: hipcc --offload-arch=gfx950 -O3 -o bench/microbench_fp28 bench/microbench_fp28.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -12,7 +13,6 @@
 #include <string.h>
 #include <vector>
 #include "../drand_amd/csrc/fp.hpp"
-#include "../drand_amd/csrc/fp_mul28.hpp"
 
 #define CHECK(x)                                                       \
   do {                                                                 \
@@ -23,71 +23,53 @@
     }                                                                  \
   } while (0)
 
-using namespace dh;  // m28:: from fp_mul28.hpp
+using namespace dh;
 
-constexpr int IT = 256;
+constexpr int IT = 512;
 
-__global__ void k_mul28(dh::fp* out, const dh::fp* in) {
-  int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  dh::fp x = in[gid & 1023], y = in[(gid + 1) & 1023], z = in[(gid + 2) & 1023];
-  for (int it = 0; it < IT; it++) {
-    m28::mul(x.v, x.v, y.v);
-    m28::mul(z.v, z.v, y.v);
-  }
-  out[gid] = dh::fp_add(x, z);
-}
-__global__ void k_mul32(dh::fp* out, const dh::fp* in) {
-  int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  dh::fp x = in[gid & 1023], y = in[(gid + 1) & 1023], z = in[(gid + 2) & 1023];
-  for (int it = 0; it < IT; it++) {
-    x = dh::fp_mul(x, y);
-    z = dh::fp_mul(z, y);
-  }
-  out[gid] = dh::fp_add(x, z);
-}
-__global__ void k_sqr28(dh::fp* out, const dh::fp* in) {
-  int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  dh::fp x = in[gid & 1023], z = in[(gid + 2) & 1023];
-  for (int it = 0; it < IT; it++) {
-    m28::sqr(x.v, x.v);
-    m28::sqr(z.v, z.v);
-  }
-  out[gid] = dh::fp_add(x, z);
-}
-__global__ void k_sqr32(dh::fp* out, const dh::fp* in) {
-  int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  dh::fp x = in[gid & 1023], z = in[(gid + 2) & 1023];
-  for (int it = 0; it < IT; it++) {
-    x = dh::fp_sqr(x);
-    z = dh::fp_sqr(z);
-  }
-  out[gid] = dh::fp_add(x, z);
+struct Mul32 { static __device__ __forceinline__ void f(fp& x, const fp& y) { fips_mont_mul(x.v, x.v, y.v); } };
+struct Mul28 { static __device__ __forceinline__ void f(fp& x, const fp& y) { m28::mul(x.v, x.v, y.v); } };
+struct Mul28i { static __device__ __forceinline__ void f(fp& x, const fp& y) { m28::mul_ilp(x.v, x.v, y.v); } };
+struct MulCall { static __device__ __forceinline__ void f(fp& x, const fp& y) { x = fp_mul(x, y); } };
+struct Sqr32 { static __device__ __forceinline__ void f(fp& x, const fp&) { fips_mont_sqr(x.v, x.v); } };
+struct Sqr28 { static __device__ __forceinline__ void f(fp& x, const fp&) { m28::sqr(x.v, x.v); } };
+struct Sqr28i { static __device__ __forceinline__ void f(fp& x, const fp&) { m28::sqr_ilp(x.v, x.v); } };
+struct SqrCall { static __device__ __forceinline__ void f(fp& x, const fp&) { x = fp_sqr(x); } };
+
+template <class Op>
+__global__ __launch_bounds__(256) void k_chain(fp* out, const fp* in) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  fp x = in[gid & 1023];
+  const fp y = in[(gid + 1) & 1023];
+#pragma unroll 1
+  for (int it = 0; it < IT; it++) Op::f(x, y);
+  out[gid] = x;
 }
 
 template <typename K>
-float time_kernel(K k, int blocks, int threads, dh::fp* out, const dh::fp* in) {
+float time_kernel(K k, int blocks, fp* out, const fp* in) {
   hipEvent_t s, e;
   (void)hipEventCreate(&s);
   (void)hipEventCreate(&e);
-  hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, 0, out, in);
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, in);
   (void)hipDeviceSynchronize();
   (void)hipEventRecord(s);
-  for (int r = 0; r < 5; r++) hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, 0, out, in);
+  for (int r = 0; r < 3; r++) hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, in);
   (void)hipEventRecord(e);
   (void)hipEventSynchronize(e);
   float ms;
   (void)hipEventElapsedTime(&ms, s, e);
-  return ms / 5;
+  return ms / 3;
 }
 
 int main() {
-  const int threads = 256, blocks = 256 * 16;
-  const size_t n = (size_t)blocks * threads;
-  dh::fp *a, *b, *in;
-  CHECK(hipMalloc(&a, n * sizeof(dh::fp)));
-  CHECK(hipMalloc(&b, n * sizeof(dh::fp)));
-  CHECK(hipMalloc(&in, 1024 * sizeof(dh::fp)));
-  dh::fp hin[1024];
+  const int max_blocks = 256 * 8;
+  const size_t n = (size_t)max_blocks * 256;
+  fp *ref, *out, *in;
+  CHECK(hipMalloc(&ref, n * sizeof(fp)));
+  CHECK(hipMalloc(&out, n * sizeof(fp)));
+  CHECK(hipMalloc(&in, 1024 * sizeof(fp)));
+  static fp hin[1024];
   uint64_t s = 0x9e3779b97f4a7c15ull;
   for (int i = 0; i < 1024; i++) {
     for (int j = 0; j < 12; j++) {
@@ -97,22 +79,30 @@ int main() {
     hin[i].v[11] &= 0x0fffffffu;  // < p
   }
   CHECK(hipMemcpy(in, hin, sizeof(hin), hipMemcpyHostToDevice));
-  const double ops = (double)n * IT * 2;
-  struct { const char* name; float ms; } r[4];
-  r[0] = {"mul32", time_kernel(k_mul32, blocks, threads, a, in)};
-  r[1] = {"mul28", time_kernel(k_mul28, blocks, threads, b, in)};
-  std::vector<dh::fp> ha(n), hb(n);
-  CHECK(hipMemcpy(ha.data(), a, n * sizeof(dh::fp), hipMemcpyDeviceToHost));
-  CHECK(hipMemcpy(hb.data(), b, n * sizeof(dh::fp), hipMemcpyDeviceToHost));
-  size_t bad_mul = 0;
-  for (size_t i = 0; i < n; i++) bad_mul += memcmp(&ha[i], &hb[i], sizeof(dh::fp)) != 0;
-  r[2] = {"sqr32", time_kernel(k_sqr32, blocks, threads, a, in)};
-  r[3] = {"sqr28", time_kernel(k_sqr28, blocks, threads, b, in)};
-  CHECK(hipMemcpy(ha.data(), a, n * sizeof(dh::fp), hipMemcpyDeviceToHost));
-  CHECK(hipMemcpy(hb.data(), b, n * sizeof(dh::fp), hipMemcpyDeviceToHost));
-  size_t bad_sqr = 0;
-  for (size_t i = 0; i < n; i++) bad_sqr += memcmp(&ha[i], &hb[i], sizeof(dh::fp)) != 0;
-  for (auto& x : r) printf("{\"op\": \"%s\", \"G_per_s\": %.2f, \"ms\": %.3f}\n", x.name, ops / x.ms / 1e6, x.ms);
-  printf("{\"mismatch_mul\": %zu, \"mismatch_sqr\": %zu, \"n\": %zu}\n", bad_mul, bad_sqr, n);
+  std::vector<fp> hr(n), ho(n);
+  struct Form {
+    const char* name;
+    void (*k)(fp*, const fp*);
+    int sq;
+  } forms[] = {{"mul32", k_chain<Mul32>, 0}, {"mul28", k_chain<Mul28>, 0}, {"mul28i", k_chain<Mul28i>, 0},
+               {"mulcall", k_chain<MulCall>, 0}, {"sqr32", k_chain<Sqr32>, 1}, {"sqr28", k_chain<Sqr28>, 1},
+               {"sqr28i", k_chain<Sqr28i>, 1}, {"sqrcall", k_chain<SqrCall>, 1}};
+  for (int wps : {1, 2, 8}) {
+    const int blocks = 256 * wps;
+    const double ops = (double)blocks * 256 * IT;
+    for (auto& f : forms) {
+      const float ms = time_kernel(f.k, blocks, out, in);
+      size_t bad = 0;
+      if (wps == 8) {  // compare with the 32-bit form of the same operation
+        hipLaunchKernelGGL(f.sq ? k_chain<Sqr32> : k_chain<Mul32>, dim3(blocks), dim3(256), 0, 0, ref, in);
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipMemcpy(hr.data(), ref, n * sizeof(fp), hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(ho.data(), out, n * sizeof(fp), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; i++) bad += memcmp(&hr[i], &ho[i], sizeof(fp)) != 0;
+      }
+      printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"G_per_s\": %.2f, \"ms\": %.3f%s%zu}\n", f.name, wps,
+             ops / ms / 1e6, ms, wps == 8 ? ", \"mismatch\": " : ", \"_\": ", bad);
+    }
+  }
   return 0;
 }

@@ -29,6 +29,7 @@ DH_DEV fp f_select(bool c, const fp& a, const fp& b) { return fp_select(c, a, b)
 DH_DEV void f_set_zero(fp& a) { a = fp_zero(); }
 DH_DEV void f_set_one(fp& a) { a = fp_one(); }
 DH_DEV fp f_inv(const fp& a) { return fp_inv(a); }
+DH_DEV fp f_inv_vt(const fp& a) { return fp_inv_vt(a); }
 
 DH_DEV fp2 f_add(const fp2& a, const fp2& b) { return fp2_add(a, b); }
 DH_DEV fp2 f_add_nr(const fp2& a, const fp2& b) { return fp2_add(a, b); }
@@ -43,6 +44,7 @@ DH_DEV fp2 f_select(bool c, const fp2& a, const fp2& b) { return fp2_select(c, a
 DH_DEV void f_set_zero(fp2& a) { a = fp2_zero(); }
 DH_DEV void f_set_one(fp2& a) { a = fp2_one(); }
 DH_DEV fp2 f_inv(const fp2& a) { return fp2_inv(a); }
+DH_DEV fp2 f_inv_vt(const fp2& a) { return fp2_inv_vt(a); }
 
 template <class F>
 struct jac {
@@ -196,6 +198,13 @@ DH_DEV jac<F> jac_mul_uabs_j(const jac<F>& p) {
 template <class F>
 DH_DEV aff<F> jac_to_aff(const jac<F>& p) {
   F zi = f_inv(p.z);
+  F zi2 = f_sqr(zi);
+  return {f_mul(p.x, zi2), f_mul(p.y, f_mul(zi2, zi))};
+}
+// the same for PUBLIC points (verification side: variable-time inversion)
+template <class F>
+DH_DEV aff<F> jac_to_aff_vt(const jac<F>& p) {
+  F zi = f_inv_vt(p.z);
   F zi2 = f_sqr(zi);
   return {f_mul(p.x, zi2), f_mul(p.y, f_mul(zi2, zi))};
 }

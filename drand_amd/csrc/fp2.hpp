@@ -50,6 +50,13 @@ DH_DEV fp2 fp2_inv(const fp2& a) {
   return {fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
 }
 
+// variable time, public inputs only (fp_inv_vt)
+DH_DEV fp2 fp2_inv_vt(const fp2& a) {
+  fp n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp ni = fp_inv_vt(n);
+  return {fp_mul(a.c0, ni), fp_neg(fp_mul(a.c1, ni))};
+}
+
 DH_DEV fp2 fp2_pow_words(const fp2& x, const uint32_t* e, int nbits) {
   fp2 acc = x;
   for (int b = nbits - 2; b >= 0; b--) {

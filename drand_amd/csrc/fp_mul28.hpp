@@ -115,5 +115,67 @@ __device__ __forceinline__ void sqr(uint32_t r[12], const uint32_t x[12]) {
 #pragma unroll
   for (int i = 0; i < 12; i++) r[i] = br ? r[i] : t[i];
 }
+// The same product with each column's sum split off the critical path: the Montgomery quotient digit Mq[k] waits only
+// for the previous digit's term Mq[k-1] * P[1] and the carry; every other term of column k (the x*y products and the
+// older digits' products) goes into two independent accumulators that the scheduler can interleave with the previous
+// column. Same terms, same bound (< 2^61), same result.
+#define M28_ILP_BODY(COL2)                                                                  \
+  uint32_t Mq[14], R[14];                                                                   \
+  uint64_t acc = 0;                                                                         \
+  _Pragma("unroll") for (int k = 0; k < 27; k++) {                                          \
+    uint64_t s0 = 0, s1 = 0;                                                                \
+    COL2(k, s0, s1);                                                                        \
+    _Pragma("unroll") for (int i = (k > 13 ? k - 13 : 0); i <= (k < 14 ? k - 2 : 13); i++) \
+      if (i & 1) s1 += (uint64_t)Mq[i] * P[k - i];                                          \
+      else s0 += (uint64_t)Mq[i] * P[k - i];                                                \
+    acc = (acc >> 28) + (s0 + s1);                                                          \
+    if (k < 14) {                                                                           \
+      if (k >= 1) acc += (uint64_t)Mq[k - 1] * P[1];                                        \
+      Mq[k] = ((uint32_t)acc * N0) & MASK;                                                  \
+      acc += (uint64_t)Mq[k] * P[0];                                                        \
+    } else {                                                                                \
+      R[k - 14] = (uint32_t)acc & MASK;                                                     \
+    }                                                                                       \
+  }                                                                                         \
+  R[13] = (uint32_t)(acc >> 28);
+
+__device__ __forceinline__ void final_sub(uint32_t r[12]) {
+  uint32_t t[12];
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; i++) t[i] = __builtin_subc(r[i], P32[i], br, &br);
+#pragma unroll
+  for (int i = 0; i < 12; i++) r[i] = br ? r[i] : t[i];
+}
+
+__device__ __forceinline__ void mul_ilp(uint32_t r[12], const uint32_t x[12], const uint32_t y[12]) {
+  uint32_t X[14], Y[14];
+  split<0>(X, x);
+  split<8>(Y, y);
+#define COLM2(k, s0, s1)                                                                     \
+  _Pragma("unroll") for (int i = ((k) > 13 ? (k) - 13 : 0); i <= ((k) < 13 ? (k) : 13); i++) \
+      if (i & 1) s1 += (uint64_t)X[i] * Y[(k) - i];                                          \
+      else s0 += (uint64_t)X[i] * Y[(k) - i];
+  M28_ILP_BODY(COLM2)
+#undef COLM2
+  join(r, R);
+  final_sub(r);
+}
+
+__device__ __forceinline__ void sqr_ilp(uint32_t r[12], const uint32_t x[12]) {
+  uint32_t X[14], X2[14];
+  split<4>(X, x);
+#pragma unroll
+  for (int i = 0; i < 14; i++) X2[i] = X[i] << 1;
+#define COLS2(k, s0, s1)                                                                                  \
+  _Pragma("unroll") for (int i = ((k) > 13 ? (k) - 13 : 0); 2 * i < (k); i++)                              \
+      if (i & 1) s1 += (uint64_t)X[i] * X2[(k) - i];                                                      \
+      else s0 += (uint64_t)X[i] * X2[(k) - i];                                                            \
+  if (((k) & 1) == 0) s1 += (uint64_t)X[(k) / 2] * X[(k) / 2];
+  M28_ILP_BODY(COLS2)
+#undef COLS2
+  join(r, R);
+  final_sub(r);
+}
 }  // namespace m28
 }  // namespace dh
