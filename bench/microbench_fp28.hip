@@ -1,8 +1,6 @@
 // Microbenchmark: Fp Montgomery products on gfx950 in the forms the library has used, at controlled occupancy.
 //   mul32 / sqr32        12 x 32-bit product scanning, inlined (fp_mul_fips.hpp: a v_addc per partial product)
 //   mul28 / sqr28        14 x 28-bit limbs, one 64-bit column accumulator chain (fp_mul28.hpp m28::mul / sqr)
-//   mul28i / sqr28i      the same with each column's off-critical-path terms in two independent accumulators
-//                        (m28::mul_ilp / sqr_ilp)
 //   call                 the library's out-of-line product (fp.hpp dh::fp_mul / fp_sqr through DH_FP_CALL)
 // Each lane runs ONE dependent chain x = x * y (or x = x^2), as a pairing program or an exponentiation does, at 1, 2
 // and 8 waves per SIMD (blocks of 256 threads = 1 wave per SIMD per CU). Every form's result is compared with mul32.
@@ -29,11 +27,9 @@ constexpr int IT = 512;
 
 struct Mul32 { static __device__ __forceinline__ void f(fp& x, const fp& y) { fips_mont_mul(x.v, x.v, y.v); } };
 struct Mul28 { static __device__ __forceinline__ void f(fp& x, const fp& y) { m28::mul(x.v, x.v, y.v); } };
-struct Mul28i { static __device__ __forceinline__ void f(fp& x, const fp& y) { m28::mul_ilp(x.v, x.v, y.v); } };
 struct MulCall { static __device__ __forceinline__ void f(fp& x, const fp& y) { x = fp_mul(x, y); } };
 struct Sqr32 { static __device__ __forceinline__ void f(fp& x, const fp&) { fips_mont_sqr(x.v, x.v); } };
 struct Sqr28 { static __device__ __forceinline__ void f(fp& x, const fp&) { m28::sqr(x.v, x.v); } };
-struct Sqr28i { static __device__ __forceinline__ void f(fp& x, const fp&) { m28::sqr_ilp(x.v, x.v); } };
 struct SqrCall { static __device__ __forceinline__ void f(fp& x, const fp&) { x = fp_sqr(x); } };
 
 template <class Op>
@@ -84,9 +80,8 @@ int main() {
     const char* name;
     void (*k)(fp*, const fp*);
     int sq;
-  } forms[] = {{"mul32", k_chain<Mul32>, 0}, {"mul28", k_chain<Mul28>, 0}, {"mul28i", k_chain<Mul28i>, 0},
-               {"mulcall", k_chain<MulCall>, 0}, {"sqr32", k_chain<Sqr32>, 1}, {"sqr28", k_chain<Sqr28>, 1},
-               {"sqr28i", k_chain<Sqr28i>, 1}, {"sqrcall", k_chain<SqrCall>, 1}};
+  } forms[] = {{"mul32", k_chain<Mul32>, 0}, {"mul28", k_chain<Mul28>, 0}, {"mulcall", k_chain<MulCall>, 0}, {"sqr32", k_chain<Sqr32>, 1}, {"sqr28", k_chain<Sqr28>, 1},
+               {"sqrcall", k_chain<SqrCall>, 1}};
   for (int wps : {1, 2, 8}) {
     const int blocks = 256 * wps;
     const double ops = (double)blocks * 256 * IT;

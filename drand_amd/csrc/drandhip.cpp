@@ -791,7 +791,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     const size_t npairs = (size_t)n_nodes + 1;
     HIP_TRY(w->r_P.ensure(npairs * JAC_WORDS_G1 * 4));
     HIP_TRY(w->r_Q.ensure(npairs * JAC_WORDS_G2 * 4));
-    HIP_TRY(w->r_f.ensure(npairs * 144 * 4));
+    HIP_TRY(w->r_f.ensure(npairs * 192 * 4));  // k_vm.hip F12_WORDS (the one-lane path uses 144)
     HIP_TRY(w->r_skip.ensure(npairs + 4));
     HIP_TRY(w->pass.ensure(16));
     HIP_TRY(T.run("recover_pair_check", [&] {

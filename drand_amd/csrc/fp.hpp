@@ -189,11 +189,7 @@ extern "C" __device__ __noinline__ __attribute__((used)) fpvec dh_fp_mul_vec(fpv
   uint32_t x[12], y[12], r[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) { x[i] = a[i]; y[i] = b[i]; }
-#ifdef DH_FP28_ILP
-  m28::mul_ilp(r, x, y);
-#else
   m28::mul(r, x, y);
-#endif
   fpvec o;
 #pragma unroll
   for (int i = 0; i < 12; i++) o[i] = r[i];
@@ -203,11 +199,7 @@ extern "C" __device__ __noinline__ __attribute__((used)) fpvec dh_fp_sqr_vec(fpv
   uint32_t x[12], r[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) x[i] = a[i];
-#ifdef DH_FP28_ILP
-  m28::sqr_ilp(r, x);
-#else
   m28::sqr(r, x);
-#endif
   fpvec o;
 #pragma unroll
   for (int i = 0; i < 12; i++) o[i] = r[i];
@@ -379,12 +371,12 @@ DH_DEV bool inv_vt_is_one(const uint32_t u[12]) {
   for (int i = 1; i < 12; i++) z |= u[i];
   return z == 0;
 }
-DH_DEV fp fp_inv_vt(const fp& a) {
-  if (fp_is_zero(a)) return a;
+// in place: a (integer in [1, p)) -> a^-1 mod p
+DH_DEV void inv_vt_int(uint32_t a[12]) {
   uint32_t u[12], v[12], x1[12], x2[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) {
-    u[i] = a.v[i];
+    u[i] = a[i];
     v[i] = p_limb(i);
     x1[i] = i == 0;
     x2[i] = 0;
@@ -428,9 +420,13 @@ DH_DEV fp fp_inv_vt(const fp& a) {
       }
     }
   }
-  fp r;
 #pragma unroll
-  for (int i = 0; i < 12; i++) r.v[i] = in_u ? x1[i] : x2[i];
+  for (int i = 0; i < 12; i++) a[i] = in_u ? x1[i] : x2[i];
+}
+DH_DEV fp fp_inv_vt(const fp& a) {
+  if (fp_is_zero(a)) return a;
+  fp r = a;
+  inv_vt_int(r.v);
   const fp r3 = {{0xd94ca1e0u, 0xed48ac6bu, 0x03a7adf8u, 0x315f831eu, 0x615e29ddu, 0x9a53352au, 0x921e1761u, 0x34c04e5eu,
                   0x65724728u, 0x2512d435u, 0x91755d4du, 0x0aa63460u}};  // R^3 mod p
   return fp_mul(r, r3);

@@ -1,20 +1,25 @@
-// Fp Montgomery product and squaring on 14 x 28-bit limbs behind the 12 x 32-bit interface of fp.hpp.
-// These are the bodies of the library's out-of-line field products (fp.hpp dh_fp_mul_vec / dh_fp_sqr_vec; call
-// clobbers v0-v39, v48-v53, s0-s17, checked at build time by drand_amd/tools/check_fp_abi.py) and of the pairing
-// VM's inlined products (k_vm.hip); bench/microbench_fp28.hip measures them against the 32-bit form.
+// Fp Montgomery product and squaring on 14 x 28-bit limbs.
+//   * mul / sqr: behind the 12 x 32-bit interface of fp.hpp — the bodies of the library's out-of-line field products
+//     (fp.hpp dh_fp_mul_vec / dh_fp_sqr_vec; call clobbers v0-v39, v48-v53, s0-s17, checked at build time by
+//     drand_amd/tools/check_fp_abi.py);
+//   * mont_mul / mont_sqr: the same reduction on values already held as 28-bit limbs, Montgomery radix R' = 2^392
+//     — the pairing VM's own representation (k_vm.hip), which skips the 12 <-> 14 limb slicing and the final
+//     subtraction.
 //
 // Why 28 bits: on gfx950 the 32-bit product-scanning step is a v_mad_u64_u32 PLUS a v_addc_co_u32 for the carry
 // into the column's third word, and the carry add issues as slowly as the multiply (~19 T MAC/s either way against
 // 37 T/s for the bare MAD, profiles/microbench_carry_r02.txt). A 28x28-bit product is < 2^56, so one 64-bit
 // accumulator absorbs a whole column (<= 28 products + the carry-in < 2^61) with ONE v_mad_u64_u32 per product
 // and no carry add: 392 MADs for a product, 301 for a squaring, plus ~25 column normalisations (mask, 64-bit
-// shift, one 28-bit v_mul_lo for the Montgomery quotient digit) and the 12 <-> 14 limb slicing.
-// Measured (bench/microbench_fp28.hip, profiles/microbench_fp28_r02.txt): 69.96 vs 59.65 G products/s, 80.74 vs
-// 67.91 G squarings/s, bit-identical results over 2^28 chained products.
+// shift, one 28-bit v_mul_lo for the Montgomery quotient digit).
+// Measured at one dependent chain per lane (bench/microbench_fp28.hip, profiles/microbench_fp28_r02b.txt): +5%
+// products and +11% squarings over the 12 x 32-bit form at 8 waves/SIMD, +7% / +22% at 1 wave/SIMD; splitting
+// each column's sum over two accumulators (more ILP) measured only +1.5-2% and was not kept.
 //
-// Same values as the 32-bit form: inputs < p, output < p, x*y / 2^384 mod p. The product slices y * 2^8 and the
-// squaring slices x * 2^4 (both < 2^392), so the 28-bit Montgomery division by R' = 2^392 leaves x*y / 2^384; the
-// result before the final subtraction is < 2p (x*y*2^8 + m*p < 2^392 * 2p).
+// mont_mul(X, Y) = X Y / 2^392 + m p / 2^392 with m < 2^392: for X, Y < 2p the result is < 4p^2/2^392 + p
+// < 1.002 p, limbs normalised (R[13] < 2^19).
+// mul(x, y) (12 x 32-bit, x, y < p): the product slices y * 2^8 and the squaring slices x * 2^4 (both < 2^392), so
+// the division by 2^392 leaves x y / 2^384, the value of the 32-bit form; one conditional subtraction gives < p.
 #pragma once
 #include <stdint.h>
 
@@ -60,7 +65,7 @@ __device__ __forceinline__ void join(uint32_t r[12], const uint32_t L[14]) {
 
 // product-scanning Montgomery reduction over the column sums given by COL(k, acc)
 #define M28_BODY(COL)                                                   \
-  uint32_t Mq[14], R[14];                                               \
+  uint32_t Mq[14];                                                      \
   uint64_t acc = 0;                                                     \
   _Pragma("unroll") for (int k = 0; k < 14; k++) {                      \
     COL(k, acc);                                                        \
@@ -77,29 +82,18 @@ __device__ __forceinline__ void join(uint32_t r[12], const uint32_t L[14]) {
   }                                                                     \
   R[13] = (uint32_t)acc;
 
-__device__ __forceinline__ void mul(uint32_t r[12], const uint32_t x[12], const uint32_t y[12]) {
-  uint32_t X[14], Y[14];
-  split<0>(X, x);
-  split<8>(Y, y);
+// R = X Y / 2^392 (mod p, < X Y / 2^392 + p)
+__device__ __forceinline__ void mont_mul(uint32_t R[14], const uint32_t X[14], const uint32_t Y[14]) {
 #define COLM(k, acc)                                                                         \
   _Pragma("unroll") for (int i = ((k) > 13 ? (k) - 13 : 0); i <= ((k) < 13 ? (k) : 13); i++) \
       acc += (uint64_t)X[i] * Y[(k) - i];
   M28_BODY(COLM)
 #undef COLM
-  join(r, R);
-  // < 2p: one conditional subtraction, as fp_mul (fips_final_sub form)
-  uint32_t t[12];
-  unsigned br = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) t[i] = __builtin_subc(r[i], P32[i], br, &br);
-#pragma unroll
-  for (int i = 0; i < 12; i++) r[i] = br ? r[i] : t[i];
 }
 
-// x^2 / 2^384 = (x 2^4)^2 / 2^392: square the limbs of x 2^4 (< 2^385) symmetrically, 105 products instead of 196
-__device__ __forceinline__ void sqr(uint32_t r[12], const uint32_t x[12]) {
-  uint32_t X[14], X2[14];
-  split<4>(X, x);
+// R = X^2 / 2^392, the off-diagonal products once against the doubled limbs: 105 products instead of 196
+__device__ __forceinline__ void mont_sqr(uint32_t R[14], const uint32_t X[14]) {
+  uint32_t X2[14];
 #pragma unroll
   for (int i = 0; i < 14; i++) X2[i] = X[i] << 1;
 #define COLS(k, acc)                                                                                  \
@@ -107,38 +101,9 @@ __device__ __forceinline__ void sqr(uint32_t r[12], const uint32_t x[12]) {
   if (((k) & 1) == 0) acc += (uint64_t)X[(k) / 2] * X[(k) / 2];
   M28_BODY(COLS)
 #undef COLS
-  join(r, R);
-  uint32_t t[12];
-  unsigned br = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) t[i] = __builtin_subc(r[i], P32[i], br, &br);
-#pragma unroll
-  for (int i = 0; i < 12; i++) r[i] = br ? r[i] : t[i];
 }
-// The same product with each column's sum split off the critical path: the Montgomery quotient digit Mq[k] waits only
-// for the previous digit's term Mq[k-1] * P[1] and the carry; every other term of column k (the x*y products and the
-// older digits' products) goes into two independent accumulators that the scheduler can interleave with the previous
-// column. Same terms, same bound (< 2^61), same result.
-#define M28_ILP_BODY(COL2)                                                                  \
-  uint32_t Mq[14], R[14];                                                                   \
-  uint64_t acc = 0;                                                                         \
-  _Pragma("unroll") for (int k = 0; k < 27; k++) {                                          \
-    uint64_t s0 = 0, s1 = 0;                                                                \
-    COL2(k, s0, s1);                                                                        \
-    _Pragma("unroll") for (int i = (k > 13 ? k - 13 : 0); i <= (k < 14 ? k - 2 : 13); i++) \
-      if (i & 1) s1 += (uint64_t)Mq[i] * P[k - i];                                          \
-      else s0 += (uint64_t)Mq[i] * P[k - i];                                                \
-    acc = (acc >> 28) + (s0 + s1);                                                          \
-    if (k < 14) {                                                                           \
-      if (k >= 1) acc += (uint64_t)Mq[k - 1] * P[1];                                        \
-      Mq[k] = ((uint32_t)acc * N0) & MASK;                                                  \
-      acc += (uint64_t)Mq[k] * P[0];                                                        \
-    } else {                                                                                \
-      R[k - 14] = (uint32_t)acc & MASK;                                                     \
-    }                                                                                       \
-  }                                                                                         \
-  R[13] = (uint32_t)(acc >> 28);
 
+// r < 2p -> r < p (12 x 32-bit words)
 __device__ __forceinline__ void final_sub(uint32_t r[12]) {
   uint32_t t[12];
   unsigned br = 0;
@@ -148,32 +113,20 @@ __device__ __forceinline__ void final_sub(uint32_t r[12]) {
   for (int i = 0; i < 12; i++) r[i] = br ? r[i] : t[i];
 }
 
-__device__ __forceinline__ void mul_ilp(uint32_t r[12], const uint32_t x[12], const uint32_t y[12]) {
-  uint32_t X[14], Y[14];
+__device__ __forceinline__ void mul(uint32_t r[12], const uint32_t x[12], const uint32_t y[12]) {
+  uint32_t X[14], Y[14], R[14];
   split<0>(X, x);
   split<8>(Y, y);
-#define COLM2(k, s0, s1)                                                                     \
-  _Pragma("unroll") for (int i = ((k) > 13 ? (k) - 13 : 0); i <= ((k) < 13 ? (k) : 13); i++) \
-      if (i & 1) s1 += (uint64_t)X[i] * Y[(k) - i];                                          \
-      else s0 += (uint64_t)X[i] * Y[(k) - i];
-  M28_ILP_BODY(COLM2)
-#undef COLM2
+  mont_mul(R, X, Y);
   join(r, R);
   final_sub(r);
 }
 
-__device__ __forceinline__ void sqr_ilp(uint32_t r[12], const uint32_t x[12]) {
-  uint32_t X[14], X2[14];
+// x^2 / 2^384 = (x 2^4)^2 / 2^392 (x 2^4 < 2^385)
+__device__ __forceinline__ void sqr(uint32_t r[12], const uint32_t x[12]) {
+  uint32_t X[14], R[14];
   split<4>(X, x);
-#pragma unroll
-  for (int i = 0; i < 14; i++) X2[i] = X[i] << 1;
-#define COLS2(k, s0, s1)                                                                                  \
-  _Pragma("unroll") for (int i = ((k) > 13 ? (k) - 13 : 0); 2 * i < (k); i++)                              \
-      if (i & 1) s1 += (uint64_t)X[i] * X2[(k) - i];                                                      \
-      else s0 += (uint64_t)X[i] * X2[(k) - i];                                                            \
-  if (((k) & 1) == 0) s1 += (uint64_t)X[(k) / 2] * X[(k) / 2];
-  M28_ILP_BODY(COLS2)
-#undef COLS2
+  mont_sqr(R, X);
   join(r, R);
   final_sub(r);
 }

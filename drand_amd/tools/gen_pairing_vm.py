@@ -14,7 +14,10 @@ M-twist, HHT final exponentiation with Granger-Scott squarings) on symbolic Fp v
 
 csrc/k_vm.hip interprets it with one wavefront per check: lane k runs op k of the current phase (one product per
 lane), phases are separated by a workgroup barrier. Additions are folded into the operands of the products that
-consume them (an operand is a linear combination of up to MAXT earlier values), so most phases are MUL phases.
+consume them (an operand is a linear combination of up to MAXT earlier values); sums stay symbolic up to MAXT_LIN
+terms and are materialised by LIN ops, larger ones as a balanced tree of LIN ops (one phase per level). Slots hold
+the VM's own representation (14 x 28-bit limbs, Montgomery radix 2^392: fp_mul28.hpp mont_mul), so the constants
+are emitted in it.
 
 The program is validated here by evaluating the scheduled, slot-allocated program in Python (the exact
 computation the device does, in the normal rather than Montgomery domain) on points from oracle/bls_py.py:
@@ -30,9 +33,11 @@ import gen_consts as gc  # noqa: E402
 
 P = gc.P
 U_ABS = -gc.U
-MAXT = 7     # terms per operand / LIN op
-MAXC = 64     # |coefficient| per term
+MAXT = 15        # terms per product operand (two operands share one op record)
+MAXT_LIN = 31    # terms per LIN op (the record's words 1..31)
+MAXC = 32767     # |coefficient| per term (16-bit signed field of a term word)
 LANES = 64
+RP = 1 << 392    # the VM's Montgomery radix (k_vm.hip: 14 x 28-bit limbs)
 
 
 # ----------------------------------------------------------------------------------------- program builder
@@ -63,6 +68,10 @@ class Prog:
     def lin(self, a):
         return self._add(kind="lin", a=a.terms_list())
 
+    def lin_terms(self, items):
+        """a LIN op from a (node, coeff) list (a node may repeat)"""
+        return self._add(kind="lin", a=list(items))
+
     def inv(self, a):
         return self._add(kind="inv", a=a.terms_list())
 
@@ -92,34 +101,40 @@ class L:
     def terms_list(self):
         return sorted(self.t.items())
 
+    def _ok(self, limit):
+        return len(self.t) <= limit and all(abs(c) <= MAXC for c in self.t.values())
+
     def _norm(self):
-        if len(self.t) <= MAXT and all(abs(c) <= MAXC for c in self.t.values()):
+        """a product operand: at most MAXT terms, else one LIN op"""
+        if self._ok(MAXT):
             return self
         return L.node(PROG.lin(self._split()))
 
     def _split(self):
-        # a LIN op may itself have at most MAXT terms of |c| <= MAXC: materialize pieces first
-        items = sorted(self.t.items())
-        fixed = {}
-        for k, c in items:
-            if abs(c) > MAXC:
-                # c * x = q * (MAXC x) + r x
-                q, r = divmod(abs(c), MAXC)
+        """at most MAXT_LIN terms of |c| <= MAXC; larger sums become a balanced tree of LIN ops (every chunk of a
+        level is independent, so a level costs one phase)"""
+        items = []
+        for k, c in sorted(self.t.items()):
+            while abs(c) > MAXC:  # never met by the tower code; kept for completeness
                 sgn = 1 if c > 0 else -1
-                base = L.node(PROG.lin(L({k: MAXC})))
-                part = L.node(PROG.lin(L({base.single(): q}))) if q > 1 else base
-                acc = {part.single(): sgn}
-                if r:
-                    acc[k] = sgn * r
-                n = PROG.lin(L(acc)) if len(acc) > 1 else part.single()
-                fixed[n] = fixed.get(n, 0) + (sgn if len(acc) == 1 else 1)
-            else:
-                fixed[k] = fixed.get(k, 0) + c
-        items = sorted(fixed.items())
-        while len(items) > MAXT:
-            head = L(dict(items[:MAXT]))
-            n = PROG.lin(head)
-            items = sorted([(n, 1)] + items[MAXT:])
+                items.append((k, sgn * MAXC))
+                c -= sgn * MAXC
+            items.append((k, c))
+        merged = {}
+        for k, c in items:  # a split coefficient keeps separate terms for the same node
+            merged.setdefault(k, []).append(c)
+        items = [(k, c) for k, cs in sorted(merged.items()) for c in cs]
+        while len(items) > MAXT_LIN:
+            nxt = []
+            for i in range(0, len(items), MAXT_LIN):
+                chunk = items[i:i + MAXT_LIN]
+                if len(chunk) == 1:
+                    nxt.append(chunk[0])
+                else:
+                    nxt.append((PROG.lin_terms(chunk), 1))
+            items = nxt
+        if len({k for k, _ in items}) != len(items):
+            return L.node(PROG.lin_terms(items))
         return L(dict(items))
 
     def single(self):
@@ -130,7 +145,8 @@ class L:
         t = dict(self.t)
         for k, v in o.t.items():
             t[k] = t.get(k, 0) + v
-        return L(t)._norm()
+        r = L(t)
+        return r if r._ok(MAXT_LIN) else L.node(PROG.lin(r._split()))
 
     def __sub__(self, o):
         return self + (-o)
@@ -680,7 +696,13 @@ def validate(np_, prog, outs, phases, slot, nslots):
 
 
 # ----------------------------------------------------------------------------------------- emission
-REC = 16  # words per op record: header, MAXT A terms, MAXT B terms (fixed positions), padding
+REC = 32  # words per op record: header, MAXT A terms, MAXT B terms (fixed positions), padding; LIN: MAXT_LIN A terms
+
+
+def c_fp28(v):
+    """an Fp constant in the VM's representation: v R' mod p as 14 x 28-bit limbs"""
+    m = v * RP % P
+    return "{" + ", ".join("0x%07xu" % ((m >> (28 * i)) & 0xfffffff) for i in range(14)) + "}"
 
 
 def emit(progs):
@@ -688,12 +710,17 @@ def emit(progs):
 
     Layout read by k_vm.hip: PHASES[2 * ph] = kind | cnt << 8, PHASES[2 * ph + 1] = index of the phase's first op;
     op k of phase ph is the REC-word record OPS[REC * (first + k) ...]: word 0 = dst slot | na << 16 | nb << 24,
-    words 1..MAXT = A terms, words 1+MAXT..2*MAXT = B terms, a term = slot | (coeff & 0xffff) << 16."""
-    assert 1 + 2 * MAXT <= REC
+    words 1..MAXT = A terms, words 1+MAXT..2*MAXT = B terms (a LIN op: words 1..MAXT_LIN = A terms), a term =
+    slot | (coeff & 0xffff) << 16. Constants are emitted in the VM's representation (c_fp28)."""
+    assert 1 + 2 * MAXT <= REC and 1 + MAXT_LIN <= REC
     lines = ["// generated by drand_amd/tools/gen_pairing_vm.py — do not edit",
              "// Lane-parallel multi-pairing check programs (see the generator's docstring).",
              "#pragma once", "#include <stdint.h>", "", "namespace dh {", "namespace vm {", ""]
-    lines.append("constexpr int MAXT = %d, MAXC = %d, REC = %d;" % (MAXT, MAXC, REC))
+    lines.append("constexpr int MAXT = %d, MAXT_LIN = %d, MAXC = %d, REC = %d;" % (MAXT, MAXT_LIN, MAXC, REC))
+    lines.append("// values in slots: v R' mod p (R' = 2^392) as 14 x 28-bit limbs, v < 2p (k_vm.hip)")
+    lines.append("__device__ __constant__ uint32_t ONE28[14] = %s;  // R' mod p" % c_fp28(1))
+    lines.append("__device__ __constant__ uint32_t RP3_28[14] = %s;  // R'^3 mod p (raw limbs)" % (
+        "{" + ", ".join("0x%07xu" % ((pow(RP, 3, P) >> (28 * i)) & 0xfffffff) for i in range(14)) + "}"))
     lines.append("enum : uint32_t { PH_MUL = 0, PH_LIN = 1, PH_INV = 2 };")
     lines.append("")
     for np_, prog, outs, phases, slot, nslots in progs:
@@ -706,6 +733,7 @@ def emit(progs):
                 n = nodes[i]
                 a = n["a"]
                 b = n.get("b", [])
+                assert len(a) <= (MAXT_LIN if kind == "lin" else MAXT) and len(b) <= MAXT
                 rec = [0] * REC
                 rec[0] = slot[i] | (len(a) << 16) | (len(b) << 24)
                 for k, (s_, c) in enumerate(a):
@@ -726,8 +754,8 @@ def emit(progs):
         lines.append("__device__ __constant__ uint32_t %s_OUTPUT_SLOT[12] = {%s};" % (tag, ", ".join(str(slot[o]) for o in outs)))
         lines.append("__device__ __constant__ uint32_t %s_CONST_SLOT[%d] = {%s};" % (
             tag, len(consts), ", ".join(str(s) for s, _ in consts)))
-        lines.append("__device__ __constant__ uint32_t %s_CONST_VAL[%d][12] = {%s};" % (
-            tag, len(consts), ", ".join(gc.c_fp(v) for _, v in consts)))
+        lines.append("__device__ __constant__ uint32_t %s_CONST_VAL[%d][14] = {%s};" % (
+            tag, len(consts), ", ".join(c_fp28(v) for _, v in consts)))
         lines.append("__device__ const uint32_t %s_PHASES[%d] = {%s};" % (tag, len(ph_words), ", ".join(map(str, ph_words))))
         lines.append("__device__ const uint32_t __attribute__((aligned(16))) %s_OPS[%d] = {%s};" % (
             tag, len(op_words), ", ".join("0x%x" % w for w in op_words)))
