@@ -309,13 +309,53 @@ DH_DEV fp fp_pow_words(const fp& x, const uint32_t* e, int nbits) {
 // x^e for a fixed exponent given as a sliding-window schedule (consts.hpp SCHED_*, w = 3):
 // table x, x^3, x^5, x^7; sched[0] = first table index, then (squarings << 8 | index), index 0xff =
 // squarings only. 378 squarings + ~105 multiplications for the 381-bit exponents (binary: ~228).
-DH_DEV fp fp_pow_sched(const fp& x, const uint32_t* sched, int len) {
-  const fp x2 = fp_sqr(x);
-  const fp t1 = fp_mul(x, x2);
-  const fp t2 = fp_mul(t1, x2);
-  const fp t3 = fp_mul(t2, x2);
+// The chain runs on 14 x 28-bit limbs in Montgomery radix R' = 2^392 (fp_mul28.hpp mont_mul / mont_sqr, inlined):
+// x R enters as x R' by one product with 2^400 mod p and leaves by one product with 2^384 mod p, so the ~480
+// products in between skip the 12 <-> 14 limb slicing and the final subtraction of the out-of-line bodies
+// (~110 of their ~610 instructions). Every intermediate value stays < 1.002 p with normalised limbs.
+struct fp28 {
+  uint32_t l[14];
+};
+DH_DEV fp28 fp28_mul(const fp28& a, const fp28& b) {
+  fp28 r;
+  m28::mont_mul(r.l, a.l, b.l);
+  return r;
+}
+DH_DEV fp28 fp28_sqr(const fp28& a) {
+  fp28 r;
+  m28::mont_sqr(r.l, a.l);
+  return r;
+}
+DH_DEV fp28 fp28_from(const fp& x) {  // x R -> x R'
+  fp28 a, c;
+  m28::split<0>(a.l, x.v);
+  const uint32_t k[14] = {0x80e6299u, 0x3500034u, 0xeb12856u, 0xdeb2699u, 0xc988670u, 0x4ef6697u, 0x70983e8u,
+                          0xa4e6fe9u, 0x3e8a053u, 0xecf271eu, 0xc20d323u, 0x6eb6385u, 0x47f1286u, 0x00156dau};  // 2^400 mod p
+#pragma unroll
+  for (int i = 0; i < 14; i++) c.l[i] = k[i];
+  return fp28_mul(a, c);
+}
+DH_DEV fp fp28_to(const fp28& a) {  // x R' -> x R, canonical
+  fp28 c;
+  const uint32_t k[14] = {0x002fffdu, 0x0900000u, 0xc000276u, 0x000bc40u, 0x8baebf4u, 0x5753c75u, 0x55f4898u,
+                          0x7052574u, 0x7ce5853u, 0x56ec6d7u, 0x71a97a2u, 0xe4935c0u, 0xec3fa80u, 0x0015f65u};  // 2^384 mod p
+#pragma unroll
+  for (int i = 0; i < 14; i++) c.l[i] = k[i];
+  const fp28 r = fp28_mul(a, c);
+  fp o;
+  m28::join(o.v, r.l);
+  m28::final_sub(o.v);
+  return o;
+}
+
+DH_DEV fp fp_pow_sched(const fp& x0, const uint32_t* sched, int len) {
+  const fp28 x = fp28_from(x0);
+  const fp28 x2 = fp28_sqr(x);
+  const fp28 t1 = fp28_mul(x, x2);
+  const fp28 t2 = fp28_mul(t1, x2);
+  const fp28 t3 = fp28_mul(t2, x2);
   auto pick = [&](uint32_t k) { return k == 0 ? x : (k == 1 ? t1 : (k == 2 ? t2 : t3)); };
-  fp acc = pick(sched[0]);
+  fp28 acc = pick(sched[0]);
   uint32_t next = sched[1];  // the tables end with a 0 entry: the read one step ahead stays in bounds
 #pragma unroll 1
   for (int i = 1; i < len; i++) {
@@ -323,10 +363,10 @@ DH_DEV fp fp_pow_sched(const fp& x, const uint32_t* sched, int len) {
     next = sched[i + 1];  // scalar load issued a whole step before its use
     const uint32_t nsq = op >> 8, k = op & 0xff;
 #pragma unroll 1
-    for (uint32_t j = 0; j < nsq; j++) acc = fp_sqr(acc);
-    if (k != 0xff) acc = fp_mul(acc, pick(k));
+    for (uint32_t j = 0; j < nsq; j++) acc = fp28_sqr(acc);
+    if (k != 0xff) acc = fp28_mul(acc, pick(k));
   }
-  return acc;
+  return fp28_to(acc);
 }
 
 DH_DEV fp fp_inv(const fp& x) { return fp_pow_sched(x, cst::SCHED_INV, cst::SCHED_INV_LEN); }
