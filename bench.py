@@ -302,7 +302,6 @@ def main():
             traffic = round(per_round * n) if per_round is not None else None
         roof = {"bound": "valu", "kernel": dom, "achieved": round(achieved / 1e12, 3), "peak": round(peak / 1e12, 3),
                 "unit": "Tmul32/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                "frac_of_mac_step": round(achieved / wm["mac_step_peak_per_s_measured"], 4),
                 "traffic_unit": "bytes per launch (WRITE_SIZE + FETCH_SIZE, PMC; FETCH doubled for this streaming-read "
                                 "kernel per MI355X_MICROARCH.md)",
                 "avg_launch_ms": round(avg_s * 1000, 3),
@@ -316,7 +315,7 @@ def main():
                   "verified beacons/sec (whole node), %s" % sch.name,
         "value": round(value, 1), "unit": "beacons/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak" if weak else "strong",
-        "vs_baseline": None, "dtype": "u32 (12x32-bit Montgomery limbs)", "data": "synthetic (GPU-signed chain, seeded key)",
+        "vs_baseline": None, "dtype": "u32 (Fp products on 14x28-bit limbs, 64-bit MAD accumulators; 12x32-bit Montgomery storage)", "data": "synthetic (GPU-signed chain, seeded key)",
         "config": {"workload": "%s batch verify of a %d-round chain, %s" % (
                        sch.name, total, "%d rounds per GPU" % n if weak else "split over %d GPU(s)" % world),
                    "scheme": sch.name, "rounds_total": total, "rounds_per_gpu": n, "global_batch": total,

@@ -206,6 +206,33 @@ extern "C" __device__ __noinline__ __attribute__((used)) fpvec dh_fp_sqr_vec(fpv
   return o;
 }
 
+// The same products on values already in the 28-bit representation (fp_mul28.hpp mont_mul / mont_sqr: 14 limbs,
+// radix 2^392, no slicing or final subtraction), for the chains that stay in it (fp28.hpp). Operands travel in 16
+// VGPRs (limbs 0-13; the backend has no 14-register class), a in v0-v15, b in v16-v31.
+typedef uint32_t fp28vec __attribute__((ext_vector_type(16)));
+extern "C" __device__ __noinline__ __attribute__((used)) fp28vec dh_fp28_mul_vec(fp28vec a, fp28vec b) {
+  uint32_t x[14], y[14], r[14];
+#pragma unroll
+  for (int i = 0; i < 14; i++) { x[i] = a[i]; y[i] = b[i]; }
+  m28::mont_mul(r, x, y);
+  fp28vec o;
+#pragma unroll
+  for (int i = 0; i < 14; i++) o[i] = r[i];
+  o[14] = o[15] = 0;
+  return o;
+}
+extern "C" __device__ __noinline__ __attribute__((used)) fp28vec dh_fp28_sqr_vec(fp28vec a) {
+  uint32_t x[14], r[14];
+#pragma unroll
+  for (int i = 0; i < 14; i++) x[i] = a[i];
+  m28::mont_sqr(r, x);
+  fp28vec o;
+#pragma unroll
+  for (int i = 0; i < 14; i++) o[i] = r[i];
+  o[14] = o[15] = 0;
+  return o;
+}
+
 #define DH_FP_CALL_CLOBBERS                                                                                    \
   "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", \
       "v48", "v49", "v50", "v51", "v52", "v53", "s0", "s1", "s2", "s3", "s4", "s5", "s6", "s7", "s8", "s9", "s10",  \

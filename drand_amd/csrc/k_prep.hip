@@ -27,8 +27,15 @@ __global__ __launch_bounds__(256, occ<F>::W) void k_prep_sig(const uint8_t* __re
   aff<F> a;
   uint8_t st;
   if constexpr (sizeof(F) == sizeof(fp)) {
-    st = g1_decompress(a, s, true);
+    // the point goes to HBM first and the subgroup test reloads it when it needs it (fp28.hpp g1_in_subgroup28)
+    st = g1_decompress(a, s, false);
+    if (st == DEC_OK) st_aff_aos<F>(sig_aff, i, a);
     if (rand_out) st_digest(rand_out + 32 * i, sha256_aligned<48>(s));
+    if (st == DEC_OK && !g1_in_subgroup28([&] { return ld_aff_aos<fp>(sig_aff, i); })) st = DEC_BAD;
+    if (st == DEC_OK) {
+      status[i] = st;
+      return;
+    }
   } else {
     st = g2_decompress(a, s, true);
     if (rand_out) st_digest(rand_out + 32 * i, sha256_aligned<96>(s));

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Build-time guard for the field-product call convention of fp.hpp (DH_FP_CALL / DH_FP_CALL_CLOBBERS).
+"""Build-time guard for the field-product call convention of fp.hpp (DH_FP_CALL / DH_FP_CALL_CLOBBERS) and fp28.hpp
+(DH_FP28_CALL_CLOBBERS).
 
 The kernels enter dh_fp_mul_vec / dh_fp_sqr_vec through an inline-asm s_swappc_b64 whose clobber list
 names exactly the registers the two bodies may touch. The bodies are ordinary compiled functions, so this
@@ -19,10 +20,12 @@ import sys
 import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-FUNCS = ("dh_fp_mul_vec", "dh_fp_sqr_vec")
-# fp.hpp DH_FP_CALL_CLOBBERS (+ the v0-v23 operands); the 28-bit bodies (fp_mul28.hpp) need no extra stripes
+FUNCS = ("dh_fp_mul_vec", "dh_fp_sqr_vec", "dh_fp28_mul_vec", "dh_fp28_sqr_vec")
+# fp.hpp DH_FP_CALL_CLOBBERS (+ the v0-v23 operands) and fp28.hpp DH_FP28_CALL_CLOBBERS (+ the v0-v31 operands)
 ALLOWED_V = {"dh_fp_mul_vec": set(range(0, 40)) | set(range(48, 54)),
-             "dh_fp_sqr_vec": set(range(0, 40)) | set(range(48, 54))}
+             "dh_fp_sqr_vec": set(range(0, 40)) | set(range(48, 54)),
+             "dh_fp28_mul_vec": set(range(0, 40)) | set(range(48, 54)),
+             "dh_fp28_sqr_vec": set(range(0, 40)) | set(range(48, 54))}
 ALLOWED_S = set(range(0, 18)) | {30, 31}
 # ranged operands (v[4:5]) end in "]", after which \b never matches: only the single-register form takes \b
 REG = re.compile(r"\b([vs])(?:\[(\d+):(\d+)\]|(\d+)\b)")
