@@ -1,0 +1,82 @@
+"""Integer model of the lazily reduced 28-bit G1 subgroup test (drand_amd/csrc/fp28.hpp), for tests/test_fp28_model.py.
+
+Every value is the integer the device holds (14 normalised 28-bit limbs, Montgomery radix R' = 2^392). mont() is
+fp_mul28.hpp mont_mul (exact integer (a b + m p) / R') and asserts the < 2p output bound the formulas rely on; lin()
+is f28_lin and asserts the result stays in [0, 2^392); the formulas follow fp28.hpp line by line (j28_dbl, j28_madd,
+j28_add, g1_in_subgroup28). Test infrastructure only.
+"""
+p=0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
+r=0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+RP=2**392; R=2**384
+pinv=pow(p,-1,RP)
+MAX=[0]
+def mont(a,b):
+    assert 0<=a<RP and 0<=b<RP
+    t=a*b
+    m=(-t*pinv)%RP
+    o=(t+m*p)//RP
+    assert o < 2*p, (a/p, b/p, o/p)
+    return o
+def lin(K,a,ca,b,cb):
+    v=ca*a+cb*b+K*p
+    assert 0<=v<RP, v/p
+    MAX[0]=max(MAX[0], v/p)
+    return v
+add=lambda a,b: lin(0,a,1,b,1)
+sub=lambda K,a,b: lin(K,a,1,b,-1)
+scale=lambda a,c: lin(0,a,c,a,0)
+ONE=RP%p
+def zero(a): o=mont(a,1); return o==0 or o==p
+def from_fp(x): # x is the normal field element
+    xr=x*R%p
+    return mont(xr, pow(2,400,p))
+def dbl(P):
+    X,Y,Z=P
+    a=mont(X,X); b=mont(Y,Y); c=mont(b,b); t=mont(add(X,b),add(X,b))
+    d=scale(lin(4,t,1,add(a,c),-1),2); e=scale(a,3); f=mont(e,e)
+    x=lin(24,f,1,d,-2); m=mont(e,sub(26,d,x)); y=lin(16,m,1,scale(c,2),-4); z=scale(mont(Y,Z),2)
+    return (x,y,z)
+def inf(): return (ONE,ONE,0)
+def madd(P,qx,qy):
+    X,Y,Z=P
+    if zero(Z): return (qx,qy,ONE)
+    z1z1=mont(Z,Z); u2=mont(qx,z1z1); s2=mont(mont(qy,Z),z1z1)
+    h=sub(26,u2,X); rr=sub(18,s2,Y)
+    if zero(h):
+        return dbl(P) if zero(rr) else inf()
+    hh=mont(h,h); i=scale(hh,4); j=mont(h,i); r2=scale(rr,2); v=mont(X,i)
+    x=lin(6,mont(r2,r2),1,add(j,scale(v,2)),-1)
+    m=mont(r2,sub(8,v,x)); y=lin(4,m,1,mont(Y,j),-2)
+    zs=add(Z,h); z=lin(4,mont(zs,zs),1,add(z1z1,hh),-1)
+    return (x,y,z)
+def jadd(P,Q):
+    X1,Y1,Z1=P; X2,Y2,Z2=Q
+    if zero(Z1): return Q
+    if zero(Z2): return P
+    z1z1=mont(Z1,Z1); z2z2=mont(Z2,Z2); u1=mont(X1,z2z2); u2=mont(X2,z1z1)
+    s1=mont(mont(Y1,Z2),z2z2); s2=mont(mont(Y2,Z1),z1z1)
+    h=sub(2,u2,u1); rr=sub(2,s2,s1)
+    if zero(h):
+        return dbl(P) if zero(rr) else inf()
+    h2=scale(h,2); i=mont(h2,h2); j=mont(h,i); r2=scale(rr,2); v=mont(u1,i)
+    x=lin(6,mont(r2,r2),1,add(j,scale(v,2)),-1)
+    m=mont(r2,sub(8,v,x)); y=lin(4,m,1,mont(s1,j),-2)
+    zs=add(Z1,Z2); zz=lin(4,mont(zs,zs),1,add(z1z1,z2z2),-1); z=mont(zz,h)
+    return (x,y,z)
+U=0xd201000000010000
+BETA=0x5f19672fdf76ce51ba69c6076a0f77eaddb3a93be6f89688de17d813620a00022e01fffffffefffe
+def insub(px,py,beta):
+    x=from_fp(px); y=from_fp(py)
+    acc=(x,y,ONE)
+    for b in range(62,-1,-1):
+        acc=dbl(acc)
+        if (U>>b)&1: acc=madd(acc,x,y)
+    t=acc
+    for b in range(62,-1,-1):
+        acc=dbl(acc)
+        if (U>>b)&1: acc=jadd(acc,t)
+    X,Y,Z=acc
+    if zero(Z): return False
+    bx=mont(from_fp(beta),x); z2=mont(Z,Z); z3=mont(z2,Z)
+    if not zero(sub(26,mont(bx,z2),X)): return False
+    return zero(add(mont(y,z3),Y))
