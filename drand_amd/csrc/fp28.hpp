@@ -86,7 +86,8 @@ DH_DEV f28 f28_lin(const f28& a, int ca, const f28& b, int cb) {
   int32_t c = 0;
 #pragma unroll
   for (int i = 0; i < 14; i++) {
-    const int32_t t = ca * (int32_t)a.l[i] + cb * (int32_t)b.l[i] + (K ? (int32_t)kp_limb<K>(i) : 0) + c;
+    int32_t t = ca * (int32_t)a.l[i] + cb * (int32_t)b.l[i] + c;
+    if constexpr (K != 0) t += (int32_t)kp_limb<K>(i);
     r.l[i] = (uint32_t)t & m28::MASK;
     c = t >> 28;
   }
