@@ -496,6 +496,27 @@ struct prep_gate {
   std::function<void()> recorded;  // host side: `done` is recorded, the next chunk may queue behind it
 };
 
+// MSM workspace of one bisection level (m entries in ngroups groups of geometry g, Jacobian width jw words)
+static int msm_workspace(worker* w, const dh::msm_geom& g, size_t m, size_t ngroups, size_t jw, dh::msm_ws& ws) {
+  const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
+  HIP_TRY(w->cnt.ensure(nk * 4));
+  HIP_TRY(w->off.ensure((nk + 1) * 4));
+  HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
+  HIP_TRY(w->list.ensure(dh::msm_entries(g, m) * 4));
+  HIP_TRY(w->buckets.ensure(2 * nk * jw * 4));
+  HIP_TRY(w->segs.ensure(2 * ngroups * g.nwin * g.nseg * jw * 4));
+  HIP_TRY(w->outA.ensure(ngroups * jw * 4));
+  HIP_TRY(w->outB.ensure(ngroups * jw * 4));
+  HIP_TRY(w->out2.ensure(2 * ngroups * jw * 4));
+  HIP_TRY(w->pass.ensure(ngroups));
+  HIP_TRY(w->part.ensure(dh::msm_part_bytes(dh::msm_entries(g, m), jw, 2)));
+  HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(dh::msm_entries(g, m))));
+  ws = dh::msm_ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
+                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>(), w->part.as<uint32_t>(),
+                  w->meta.as<uint32_t>(), 0};
+  return DH_OK;
+}
+
 int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                 size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
                 uint8_t* d_verdict, uint8_t* d_rand, uint64_t seed, hipStream_t st, uint64_t* stats,
@@ -512,6 +533,9 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   const size_t aw = jw * 2 / 3;
 
   timed_launches T(st);
+  bool presorted = false;  // level-0 sorted lists already built on the tail stream
+  dh::msm_geom g0{};
+  dh::msm_ws ws0{};
   if (mode <= VM_BEGIN) {
     // key
     HIP_TRY(w->key_raw.ensure(96));
@@ -536,6 +560,25 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(w->q_pts.ensure(2 * n * jw * 4));
     HIP_TRY(w->scal.ensure(n * 16));
     HIP_TRY(w->entries.ensure(n * 4));
+    uint32_t seedw[8];
+    int rc = make_seed(seed, seedw);
+    if (rc) return rc;
+    uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
+    // The level-0 sort needs only the scalars, and the scalars only the seed: with a tail stream it runs there
+    // while the per-round kernels decode and hash (its ~1 ms of small kernels left the one-call latency path).
+    // Every round then carries a scalar; the bucket passes skip rounds whose status is not DEC_OK.
+    presorted = w->tail && st == w->stream;
+    if (presorted) {
+      hipStream_t ts = w->tail;
+      HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, ts));
+      HIP_TRY(dh::launch_scalars(d_seed, n, nullptr, w->scal.as<uint4>(), 1, ts));
+      HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, ts));
+      g0 = geom_for(n, true);
+      g0.half_stride = (uint32_t)n;
+      rc = msm_workspace(w, g0, n, 1, jw, ws0);
+      if (rc) return rc;
+      HIP_TRY(dh::launch_msm_sort(g0, w->entries.as<uint32_t>(), nullptr, nullptr, n, 1, w->scal.as<uint4>(), ws0, ts));
+    }
     if (gate && gate->wait) HIP_TRY(hipStreamWaitEvent(st, gate->wait, 0));
     HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>" : "k_prep_sig<fp>", [&] {
       return dh::launch_prep(g2, d_sigs, sig_stride, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), d_rand, st);
@@ -548,12 +591,10 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
                              scheme == DH_SCHEME_CHAINED && d_prevs && !d_msgs32 ? 1 : 0, dst_id(scheme), w->status.as<uint8_t>(),
                              w->q_pts.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), st);
     }));
-    uint32_t seedw[8];
-    int rc = make_seed(seed, seedw);
-    if (rc) return rc;
-    uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
-    HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
-    HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), 1, st));
+    if (!presorted) {
+      HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
+      HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), 1, st));
+    }
     HIP_TRY(dh::launch_endo(g2, n, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(), st));
     HIP_TRY(hipMemsetAsync(d_verdict, 0, n, st));
     if (gate) {
@@ -568,7 +609,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
       w->cached_key_ok = key_ok;
     }
     if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
-    HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
+    if (!presorted) HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
   }
   // the tail (MSM, checks, bisection) runs on the worker's high-priority stream, after the per-round kernels
   if (w->tail && st == w->stream) {
@@ -596,26 +637,20 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     dh::msm_geom g = geom_for(gsize, true);
     g.half_stride = (uint32_t)n;
     const size_t ngroups = (m + gsize - 1) / gsize;
-    const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
-    HIP_TRY(w->cnt.ensure(nk * 4));
-    HIP_TRY(w->off.ensure((nk + 1) * 4));
-    HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
-    HIP_TRY(w->list.ensure(dh::msm_entries(g, m) * 4));
-    HIP_TRY(w->buckets.ensure(2 * nk * jw * 4));
-    HIP_TRY(w->segs.ensure(2 * ngroups * g.nwin * g.nseg * jw * 4));
-    HIP_TRY(w->outA.ensure(ngroups * jw * 4));
-    HIP_TRY(w->outB.ensure(ngroups * jw * 4));
-    HIP_TRY(w->out2.ensure(2 * ngroups * jw * 4));
-    HIP_TRY(w->pass.ensure(ngroups));
-    HIP_TRY(w->part.ensure(dh::msm_part_bytes(dh::msm_entries(g, m), jw, 2)));
-    HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(dh::msm_entries(g, m))));
-    dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
-                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>(), w->part.as<uint32_t>(),
-                  w->meta.as<uint32_t>(), 0};
+    const bool pre = level == 0 && presorted;
+    dh::msm_ws ws{};
+    if (pre) {
+      ws = ws0;
+    } else {
+      const int rc = msm_workspace(w, g, m, ngroups, jw, ws);
+      if (rc) return rc;
+    }
     if (!(level == 0 && mode >= VM_FINISH)) {  // a resumed batch has its level-0 sums from dh_batch_begin
+      // every level skips the rounds whose status is not DEC_OK (their scalars are nonzero after a presort)
       HIP_TRY(T.run(msm_names[std::min(level, 7)], [&] {
-        return dh::launch_msm(g2, g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(), w->sig_aff.as<uint32_t>(),
-                              w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st);
+        return dh::launch_msm(g2, pre ? g0 : g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(),
+                              w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
+                              w->outB.as<uint32_t>(), st, w->status.as<uint8_t>(), pre);
       }));
     }
     if (level == 0 && mode == VM_BEGIN) {

@@ -162,11 +162,15 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
 // (Z = 0, infinity) value the launcher writes first.
 constexpr uint32_t NO_KEY = 0xffffffffu;
 
+// skip (optional): per-round status; an entry whose round (point index mod nround: the endomorphism images follow
+// the points) is not DEC_OK adds nothing — the batch check sorts before the rounds are decoded (verify_core), so
+// such rounds carry nonzero scalars
 template <class F, bool AFFINE>
 __global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket(const uint32_t* __restrict__ off, const uint32_t* __restrict__ list,
                                                     size_t nkeys, uint32_t L, const uint32_t* __restrict__ pts,
                                                     uint32_t* __restrict__ buckets, uint32_t* __restrict__ part,
-                                                    uint32_t* __restrict__ meta) {
+                                                    uint32_t* __restrict__ meta, const uint8_t* __restrict__ skip,
+                                                    uint32_t nround) {
   const size_t t = gtid();
   const uint32_t total = off[nkeys];
   const size_t s = t * (size_t)L;
@@ -189,14 +193,16 @@ __global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket(const uint32_t* _
     const uint32_t raw = list[j];
     const uint32_t idx = raw & ~NEG_BIT;
     const bool neg = (raw & NEG_BIT) != 0;
-    if constexpr (AFFINE) {
-      aff<F> pt = ld_aff_aos<F>(pts, idx);
-      pt.y = f_select(neg, f_neg(pt.y), pt.y);
-      acc = jac_add_aff(acc, pt);
-    } else {
-      jac<F> pt = ld_jac_aos<F>(pts, idx);
-      pt.y = f_select(neg, f_neg(pt.y), pt.y);
-      acc = jac_add(acc, pt);
+    if (!skip || skip[idx < nround ? idx : idx - nround] == DEC_OK) {
+      if constexpr (AFFINE) {
+        aff<F> pt = ld_aff_aos<F>(pts, idx);
+        pt.y = f_select(neg, f_neg(pt.y), pt.y);
+        acc = jac_add_aff(acc, pt);
+      } else {
+        jac<F> pt = ld_jac_aos<F>(pts, idx);
+        pt.y = f_select(neg, f_neg(pt.y), pt.y);
+        acc = jac_add(acc, pt);
+      }
     }
     const bool ends = j + 1 == kend;
     if (ends || j + 1 == e) {
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket_fix(const uint32_
 
 template <class F, bool AFFINE>
 static hipError_t launch_buckets(const msm_ws& ws, size_t nk, const uint32_t* pts, uint32_t* buckets, uint32_t* part,
-                                 bool write_meta, hipStream_t st) {
+                                 bool write_meta, hipStream_t st, const uint8_t* skip = nullptr, uint32_t nround = 0) {
   constexpr size_t jw = sizeof(F) / 4 * 3;
   hipError_t e = hipMemsetAsync(buckets, 0, nk * jw * 4, st);
   if (e != hipSuccess) return e;
@@ -254,7 +260,7 @@ static hipError_t launch_buckets(const msm_ws& ws, size_t nk, const uint32_t* pt
   const uint32_t L = msm_chunk_len(ws.max_entries);
   const size_t nch = (ws.max_entries + L - 1) / L;  // <= msm_nchunks(max_entries): the workspace bound
   hipLaunchKernelGGL((k_msm_bucket<F, AFFINE>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, pts, buckets,
-                     part, write_meta ? ws.meta : nullptr);
+                     part, write_meta ? ws.meta : nullptr, skip, nround);
   hipLaunchKernelGGL((k_msm_bucket_fix<F>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, nk, L, ws.meta, part, buckets);
   return hipGetLastError();
 }
@@ -416,21 +422,21 @@ hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngrou
 // threads in every latency-bound reduction step instead of two serial passes).
 hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
                       const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
-                      hipStream_t st) {
-  hipError_t e = launch_msm_sort(g, entries, nullptr, nullptr, m, ngroups, scal, ws, st);
-  if (e != hipSuccess) return e;
+                      hipStream_t st, const uint8_t* skip, bool presorted) {
+  hipError_t e = hipSuccess;
+  if (!presorted && (e = launch_msm_sort(g, entries, nullptr, nullptr, m, ngroups, scal, ws, st)) != hipSuccess) return e;
   const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
   const size_t jw = sig_g2 ? 72 : 36;
   uint32_t* bB = ws.buckets + nk * jw;
   // the partial sums of the two point sets sit back to back; the chunk metadata is the same for both
   uint32_t* pB = ws.part + msm_nchunks(ws.max_entries) * 2 * jw;
   if (sig_g2) {
-    if ((e = launch_buckets<fp2, true>(ws, nk, sig_aff, ws.buckets, ws.part, true, st)) != hipSuccess) return e;
-    if ((e = launch_buckets<fp2, false>(ws, nk, q_pts, bB, pB, false, st)) != hipSuccess) return e;
+    if ((e = launch_buckets<fp2, true>(ws, nk, sig_aff, ws.buckets, ws.part, true, st, skip, g.half_stride)) != hipSuccess) return e;
+    if ((e = launch_buckets<fp2, false>(ws, nk, q_pts, bB, pB, false, st, skip, g.half_stride)) != hipSuccess) return e;
     e = msm_reduce<fp2>(g, 2 * ngroups, ws.buckets, ws.segs, ws.out2, st);
   } else {
-    if ((e = launch_buckets<fp, true>(ws, nk, sig_aff, ws.buckets, ws.part, true, st)) != hipSuccess) return e;
-    if ((e = launch_buckets<fp, false>(ws, nk, q_pts, bB, pB, false, st)) != hipSuccess) return e;
+    if ((e = launch_buckets<fp, true>(ws, nk, sig_aff, ws.buckets, ws.part, true, st, skip, g.half_stride)) != hipSuccess) return e;
+    if ((e = launch_buckets<fp, false>(ws, nk, q_pts, bB, pB, false, st, skip, g.half_stride)) != hipSuccess) return e;
     e = msm_reduce<fp>(g, 2 * ngroups, ws.buckets, ws.segs, ws.out2, st);
   }
   if (e != hipSuccess) return e;

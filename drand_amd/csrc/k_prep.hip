@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void k_scalars(const uint32_t* __restrict__ se
   // G2, |mu| > 2^63, so distinct (a, b) give distinct scalars: soundness error 2^-126 per group)
   uint4 r = glv ? make_uint4(s.h[3], s.h[2] & 0x7fffffffu, s.h[1], s.h[0] & 0x7fffffffu)
                 : make_uint4(s.h[3], s.h[2], s.h[1], s.h[0] & 0x7fffffffu);
-  if (status[i] != DEC_OK) r = make_uint4(0, 0, 0, 0);
+  if (status && status[i] != DEC_OK) r = make_uint4(0, 0, 0, 0);
   scal[i] = r;
 }
 

@@ -57,7 +57,8 @@ size_t hash_tmp_bytes(int sig_g2, size_t n);
 hipError_t launch_hash(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
                        const uint8_t* msgs32, size_t n, int chained, int dst_id, uint8_t* status, uint32_t* q_out, uint32_t* tmp,
                        hipStream_t st);
-// RLC scalars from SHA-256(seed || i): 127-bit (glv = 0) or a pair of 63-bit halves (glv = 1, msm_geom.halves = 2)
+// RLC scalars from SHA-256(seed || i): 127-bit (glv = 0) or a pair of 63-bit halves (glv = 1, msm_geom.halves = 2);
+// 0 for rounds whose status is not DEC_OK (status null: every round gets its scalar)
 hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, int glv, hipStream_t st);
 // endomorphism images for the split MSM: sig_aff[n + i] = endo(sig_aff[i]), q_pts[n + i] = endo(q_pts[i])
 // (G1: phi(x, y) = (beta x, y); G2: psi), so the sorted lists address them as point n + i
@@ -65,9 +66,11 @@ hipError_t launch_endo(int sig_g2, size_t n, uint32_t* sig_aff, uint32_t* q_pts,
 hipError_t launch_decode_key(int key_g2, const uint8_t* pk, uint32_t* key_aff, uint8_t* ok, hipStream_t st);
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t st);
 hipError_t launch_scan(const uint32_t* cnt, size_t nk, uint32_t* off, uint32_t* tmp, hipStream_t st);
+// skip (optional): per-round status, entries of rounds not DEC_OK add nothing (point index mod g.half_stride);
+// presorted: the sorted lists of (entries, scal) are already in ws (launch_msm_sort on the same geometry)
 hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
                       const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
-                      hipStream_t st);
+                      hipStream_t st, const uint8_t* skip = nullptr, bool presorted = false);
 hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp, size_t m,
                            size_t ngroups, const uint4* scal, msm_ws& ws, hipStream_t st);
 hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngroups, const uint32_t* pts, msm_ws& ws,
