@@ -5,7 +5,7 @@
 #include <stdint.h>
 #include <string.h>
 #include "../drand_amd/csrc/fp.hpp"
-#include "../drand_amd/csrc/fp_mul_fips.hpp"
+#include "fp32/fp_mul_fips.hpp"
 
 constexpr int IT = 256;
 __global__ void k_cios(dh::fp* out, const dh::fp* in) {

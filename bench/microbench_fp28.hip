@@ -1,5 +1,5 @@
 // Microbenchmark: Fp Montgomery products on gfx950 in the forms the library has used, at controlled occupancy.
-//   mul32 / sqr32        12 x 32-bit product scanning, inlined (fp_mul_fips.hpp: a v_addc per partial product)
+//   mul32 / sqr32        12 x 32-bit product scanning, inlined (bench/fp32/fp_mul_fips.hpp: a v_addc per partial product)
 //   mul28 / sqr28        14 x 28-bit limbs, one 64-bit column accumulator chain (fp_mul28.hpp m28::mul / sqr)
 //   call                 the library's out-of-line product (fp.hpp dh::fp_mul / fp_sqr through DH_FP_CALL)
 // Each lane runs ONE dependent chain x = x * y (or x = x^2), as a pairing program or an exponentiation does, at 1, 2
@@ -11,6 +11,7 @@
 #include <string.h>
 #include <vector>
 #include "../drand_amd/csrc/fp.hpp"
+#include "fp32/fp_mul_fips.hpp"
 
 #define CHECK(x)                                                       \
   do {                                                                 \

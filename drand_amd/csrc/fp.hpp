@@ -11,7 +11,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "consts.hpp"
-#include "fp_mul_fips.hpp"
 #include "fp_mul28.hpp"
 
 namespace dh {
@@ -98,7 +97,8 @@ DH_DEV fp fp_add(const fp& a, const fp& b) {
 }
 
 // a + b WITHOUT the reduction, for operands that only feed a Montgomery product: a, b < p gives a sum < 2p, and
-// the product (fp_mul_fips.hpp) is exact and fully reduced for inputs < 2p because 4p < R = 2^384
+// the product (fp_mul28.hpp mul) is exact and fully reduced for inputs < 2p: before its one conditional
+// subtraction it is < x y / 2^384 + p < 2p
 // (t = (xy + mp) / R < 4p^2/R + p < 2p before its one conditional subtraction).
 DH_DEV fp fp_add_nr(const fp& a, const fp& b) {
   fp r;
@@ -169,7 +169,7 @@ DH_DEV fp fp_mul_cios(const fp& a, const fp& b) {
 
 // The field product used everywhere: product-scanning Montgomery on 14 x 28-bit limbs behind the 12 x 32-bit
 // interface (fp_mul28.hpp: one v_mad_u64_u32 per partial product, no carry adds; the 32-bit form of
-// fp_mul_fips.hpp needs a v_addc per product and measured 17% slower), one out-of-line copy
+// bench/fp32/fp_mul_fips.hpp needs a v_addc per product and measured slower), one out-of-line copy
 // per code object so that the large kernels (pairing, hash-to-curve) stay compact; define DH_MUL_INLINE to
 // inline it instead.
 //
@@ -258,7 +258,7 @@ DH_DEV fp from_vec(const fpvec& v) {
 DH_DEV fp fp_mul(const fp& a, const fp& b) {
 #ifdef DH_MUL_INLINE
   fp r;
-  fips_mont_mul(r.v, a.v, b.v);
+  m28::mul(r.v, a.v, b.v);
   return r;
 #else
   fpvec x = to_vec(a), y = to_vec(b);
@@ -270,7 +270,7 @@ DH_DEV fp fp_mul(const fp& a, const fp& b) {
 DH_DEV fp fp_sqr(const fp& a) {
 #ifdef DH_MUL_INLINE
   fp r;
-  fips_mont_sqr(r.v, a.v);
+  m28::sqr(r.v, a.v);
   return r;
 #else
   fpvec x = to_vec(a);
