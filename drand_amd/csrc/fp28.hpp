@@ -78,8 +78,9 @@ DH_KP(26, 0xff7555eu, 0xe5fffffu, 0x7fff8e3u, 0xffde028u, 0xfab1d77u, 0x590df8fu
       0xaf8de03u, 0xf0882d5u, 0x6baba0cu, 0x1c9d6fdu, 0x02a41bdu)
 #undef DH_KP
 
-// ca a + cb b + K p limb-wise with one signed carry pass (|ca|, |cb| <= 4 keeps every limb sum inside int32; the
-// caller's bounds keep the value in [0, 2^392))
+// ca a + cb b + K p limb-wise with one signed carry pass. The negative coefficients add up to >= -8 and the positive
+// ones to <= 6, so every limb sum stays inside int32 (limbs < 2^28: a sum is >= -8 (2^28 - 1) - 8 carry); the
+// caller's bounds keep the value in [0, 2^392)
 template <int K>
 DH_DEV f28 f28_lin(const f28& a, int ca, const f28& b, int cb) {
   f28 r;
@@ -87,6 +88,20 @@ DH_DEV f28 f28_lin(const f28& a, int ca, const f28& b, int cb) {
 #pragma unroll
   for (int i = 0; i < 14; i++) {
     int32_t t = ca * (int32_t)a.l[i] + cb * (int32_t)b.l[i] + c;
+    if constexpr (K != 0) t += (int32_t)kp_limb<K>(i);
+    r.l[i] = (uint32_t)t & m28::MASK;
+    c = t >> 28;
+  }
+  return r;
+}
+// ca a + cb b + cc c + K p (same limits on the coefficients as f28_lin)
+template <int K>
+DH_DEV f28 f28_lin3(const f28& a, int ca, const f28& b, int cb, const f28& c3, int cc) {
+  f28 r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 14; i++) {
+    int32_t t = ca * (int32_t)a.l[i] + cb * (int32_t)b.l[i] + cc * (int32_t)c3.l[i] + c;
     if constexpr (K != 0) t += (int32_t)kp_limb<K>(i);
     r.l[i] = (uint32_t)t & m28::MASK;
     c = t >> 28;
@@ -142,13 +157,13 @@ DH_DEV j28 j28_dbl(const j28& p) {
   const f28 b = f28_sqr(p.y);                                          // < 2
   const f28 c = f28_sqr(b);                                            // < 2
   const f28 t = f28_sqr(f28_add(p.x, b));                              // (X + B)^2, X + B < 50
-  const f28 d = f28_scale(f28_lin<4>(t, 1, f28_add(a, c), -1), 2);    // D = 2 (T + 4p - A - C) < 12
+  const f28 d = f28_lin3<8>(t, 2, a, -2, c, -2);                       // D = 2 (T + 4p - A - C) < 12
   const f28 e = f28_scale(a, 3);                                       // E = 3A < 6
   const f28 f = f28_sqr(e);                                            // < 2
   j28 r;
   r.x = f28_lin<24>(f, 1, d, -2);                                      // F + 24p - 2D < 26
   const f28 m = f28_mul(e, f28_sub<26>(d, r.x));                       // E (D + 26p - X3): 6 x 38 -> < 2
-  r.y = f28_lin<16>(m, 1, f28_scale(c, 2), -4);                        // M + 16p - 8C < 18
+  r.y = f28_lin<16>(m, 1, c, -8);                                      // M + 16p - 8C < 18
   r.z = f28_scale(f28_mul(p.y, p.z), 2);                               // < 4
   return r;
 }
@@ -180,10 +195,10 @@ DH_DEV j28 j28_madd(const j28& p, const f28& qx, const f28& qy) {
   const f28 r2 = f28_scale(rr, 2);                                     // < 40
   const f28 v = f28_mul(p.x, i);                                       // 26 x 8 -> < 2
   j28 r;
-  r.x = f28_lin<6>(f28_sqr(r2), 1, f28_add(j, f28_scale(v, 2)), -1);  // R^2 + 6p - J - 2V < 8
+  r.x = f28_lin3<6>(f28_sqr(r2), 1, j, -1, v, -2);                    // R^2 + 6p - J - 2V < 8
   const f28 m = f28_mul(r2, f28_sub<8>(v, r.x));                       // 40 x 10 -> < 2
   r.y = f28_lin<4>(m, 1, f28_mul(p.y, j), -2);                         // < 6
-  r.z = f28_lin<4>(f28_sqr(f28_add(p.z, h)), 1, f28_add(z1z1, hh), -1);  // (Z + H)^2, Z + H < 34 -> < 6
+  r.z = f28_lin3<4>(f28_sqr(f28_add(p.z, h)), 1, z1z1, -1, hh, -1);    // (Z + H)^2, Z + H < 34 -> < 6
   return r;
 }
 
@@ -206,10 +221,10 @@ DH_DEV j28 j28_add(const j28& p, const j28& q) {
   const f28 r2 = f28_scale(rr, 2);                                     // < 8
   const f28 v = f28_mul(u1, i);                                        // < 2
   j28 r;
-  r.x = f28_lin<6>(f28_sqr(r2), 1, f28_add(j, f28_scale(v, 2)), -1);  // < 8
+  r.x = f28_lin3<6>(f28_sqr(r2), 1, j, -1, v, -2);                    // < 8
   const f28 m = f28_mul(r2, f28_sub<8>(v, r.x));                       // 8 x 10 -> < 2
   r.y = f28_lin<4>(m, 1, f28_mul(s1, j), -2);                          // < 6
-  const f28 zz = f28_lin<4>(f28_sqr(f28_add(p.z, q.z)), 1, f28_add(z1z1, z2z2), -1);  // < 6
+  const f28 zz = f28_lin3<4>(f28_sqr(f28_add(p.z, q.z)), 1, z1z1, -1, z2z2, -1);  // < 6
   r.z = f28_mul(zz, h);                                                // 6 x 4 -> < 2
   return r;
 }

@@ -22,6 +22,11 @@ def lin(K,a,ca,b,cb):
     assert 0<=v<RP, v/p
     MAX[0]=max(MAX[0], v/p)
     return v
+def lin3(K,a,ca,b,cb,c,cc):
+    v=ca*a+cb*b+cc*c+K*p
+    assert 0<=v<RP, v/p
+    MAX[0]=max(MAX[0], v/p)
+    return v
 add=lambda a,b: lin(0,a,1,b,1)
 sub=lambda K,a,b: lin(K,a,1,b,-1)
 scale=lambda a,c: lin(0,a,c,a,0)
@@ -33,8 +38,8 @@ def from_fp(x): # x is the normal field element
 def dbl(P):
     X,Y,Z=P
     a=mont(X,X); b=mont(Y,Y); c=mont(b,b); t=mont(add(X,b),add(X,b))
-    d=scale(lin(4,t,1,add(a,c),-1),2); e=scale(a,3); f=mont(e,e)
-    x=lin(24,f,1,d,-2); m=mont(e,sub(26,d,x)); y=lin(16,m,1,scale(c,2),-4); z=scale(mont(Y,Z),2)
+    d=lin3(8,t,2,a,-2,c,-2); e=scale(a,3); f=mont(e,e)
+    x=lin(24,f,1,d,-2); m=mont(e,sub(26,d,x)); y=lin(16,m,1,c,-8); z=scale(mont(Y,Z),2)
     return (x,y,z)
 def inf(): return (ONE,ONE,0)
 def madd(P,qx,qy):
@@ -45,9 +50,9 @@ def madd(P,qx,qy):
     if zero(h):
         return dbl(P) if zero(rr) else inf()
     hh=mont(h,h); i=scale(hh,4); j=mont(h,i); r2=scale(rr,2); v=mont(X,i)
-    x=lin(6,mont(r2,r2),1,add(j,scale(v,2)),-1)
+    x=lin3(6,mont(r2,r2),1,j,-1,v,-2)
     m=mont(r2,sub(8,v,x)); y=lin(4,m,1,mont(Y,j),-2)
-    zs=add(Z,h); z=lin(4,mont(zs,zs),1,add(z1z1,hh),-1)
+    zs=add(Z,h); z=lin3(4,mont(zs,zs),1,z1z1,-1,hh,-1)
     return (x,y,z)
 def jadd(P,Q):
     X1,Y1,Z1=P; X2,Y2,Z2=Q
@@ -59,9 +64,9 @@ def jadd(P,Q):
     if zero(h):
         return dbl(P) if zero(rr) else inf()
     h2=scale(h,2); i=mont(h2,h2); j=mont(h,i); r2=scale(rr,2); v=mont(u1,i)
-    x=lin(6,mont(r2,r2),1,add(j,scale(v,2)),-1)
+    x=lin3(6,mont(r2,r2),1,j,-1,v,-2)
     m=mont(r2,sub(8,v,x)); y=lin(4,m,1,mont(s1,j),-2)
-    zs=add(Z1,Z2); zz=lin(4,mont(zs,zs),1,add(z1z1,z2z2),-1); z=mont(zz,h)
+    zs=add(Z1,Z2); zz=lin3(4,mont(zs,zs),1,z1z1,-1,z2z2,-1); z=mont(zz,h)
     return (x,y,z)
 U=0xd201000000010000
 BETA=0x5f19672fdf76ce51ba69c6076a0f77eaddb3a93be6f89688de17d813620a00022e01fffffffefffe
