@@ -36,15 +36,8 @@ DH_DEV void be48_words(uint32_t out[12], const uint8_t* in, bool mask_flags) {
 }
 
 DH_DEV bool g1_in_subgroup(const aff<fp>& p) {
-  // t = [u^2] P = [|u|]([|u|] P); need phi(P) == -t. Run on lazily reduced 28-bit limbs (fp28.hpp); the
-  // 12 x 32-bit form of the same test is g1_in_subgroup32
+  // t = [u^2] P = [|u|]([|u|] P); need phi(P) == -t. Run on lazily reduced 28-bit limbs (fp28.hpp)
   return g1_in_subgroup28([&] { return p; });
-}
-DH_DEV bool g1_in_subgroup32(const aff<fp>& p) {
-  jac<fp> t = jac_mul_uabs(p);
-  t = jac_mul_uabs_j(t);
-  jac<fp> phi = jac_from_aff(aff<fp>{fp_mul(p.x, fp_c(cst::BETA)), p.y});
-  return jac_eq(phi, jac_neg(t));
 }
 
 DH_DEV bool g2_in_subgroup(const aff<fp2>& p) {

@@ -405,16 +405,18 @@ static hipError_t group_check(worker* w, bool g2, const uint32_t* A, const uint3
                                    w->vm_live.as<uint8_t>(), pass, st);
 }
 
+// key_h as for group_check: the leaves of G1-signature schemes pair the uncleared hash point with [h_eff] pk
 static hipError_t leaf_check(worker* w, bool g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff,
                              const uint32_t* q_pts, const uint32_t* key, const uint8_t* status, uint8_t* verdict,
-                             hipStream_t st) {
+                             hipStream_t st, const uint32_t* key_h = nullptr) {
   if (lane_pairing()) return dh::launch_leaf_check(g2, entries, m, sig_aff, q_pts, key, status, verdict, st);
   hipError_t e;
   if ((e = w->vm_pairs.ensure(m * 2 * 72 * 4)) != hipSuccess) return e;
   if ((e = w->vm_live.ensure(m * 2)) != hipSuccess) return e;
   if ((e = w->vm_done.ensure(m)) != hipSuccess) return e;
-  return dh::launch_leaf_check_vm(g2, entries, m, sig_aff, q_pts, key, status, w->vm_pairs.as<uint32_t>(),
-                                  w->vm_live.as<uint8_t>(), w->vm_done.as<uint8_t>(), verdict, st);
+  return dh::launch_leaf_check_vm(g2, entries, m, sig_aff, q_pts, key, g2 ? nullptr : key_h, status,
+                                  w->vm_pairs.as<uint32_t>(), w->vm_live.as<uint8_t>(), w->vm_done.as<uint8_t>(), verdict,
+                                  st);
 }
 
 // Bisection ladder. DRANDHIP_BISECT="4096,256,16,2" fixes the group sizes after level 0 (tests, experiments);
@@ -695,7 +697,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (m > 0) {
     HIP_TRY(T.run("k_leaf_check", [&] {
       return leaf_check(w, g2, w->entries.as<uint32_t>(), m, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
-                        w->key_aff.as<uint32_t>(), w->status.as<uint8_t>(), d_verdict, st);
+                        w->key_aff.as<uint32_t>(), w->status.as<uint8_t>(), d_verdict, st, w->key_aff.as<uint32_t>() + 48);
     }));
     if (stats) stats[2] = m;
   }

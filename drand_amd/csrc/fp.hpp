@@ -322,17 +322,6 @@ DH_DEV fp fp_c(const uint32_t* c) {
 
 DH_DEV fp fp_mul_c(const fp& a, const uint32_t* c) { return fp_mul(a, fp_c(c)); }
 
-// x^e for a public exponent held as little-endian 32-bit words (uniform across lanes, so
-// the multiply branch is a scalar branch: no divergence).
-DH_DEV fp fp_pow_words(const fp& x, const uint32_t* e, int nbits) {
-  fp acc = x;  // top bit is 1
-  for (int b = nbits - 2; b >= 0; b--) {
-    acc = fp_sqr(acc);
-    if ((e[b >> 5] >> (b & 31)) & 1) acc = fp_mul(acc, x);
-  }
-  return acc;
-}
-
 // x^e for a fixed exponent given as a sliding-window schedule (consts.hpp SCHED_*, w = 3):
 // table x, x^3, x^5, x^7; sched[0] = first table index, then (squarings << 8 | index), index 0xff =
 // squarings only. 378 squarings + ~105 multiplications for the 381-bit exponents (binary: ~228).

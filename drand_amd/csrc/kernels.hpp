@@ -90,8 +90,8 @@ hipError_t launch_group_check_vm(int sig_g2, const uint32_t* A, const uint32_t* 
                                  const uint32_t* key_h,
                                  uint32_t* pairs, uint8_t* live, uint8_t* pass, hipStream_t st);
 hipError_t launch_leaf_check_vm(int sig_g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
-                                const uint32_t* key_aff, const uint8_t* status, uint32_t* pairs, uint8_t* live, uint8_t* done,
-                                uint8_t* verdict, hipStream_t st);
+                                const uint32_t* key_aff, const uint32_t* key_h, const uint8_t* status, uint32_t* pairs,
+                                uint8_t* live, uint8_t* done, uint8_t* verdict, hipStream_t st);
 
 hipError_t launch_multi_pairing_vm(const uint32_t* P, const uint32_t* Q, size_t n, uint32_t* pairs, uint8_t* live,
                                    uint32_t* f_tmp, uint8_t* pass, hipStream_t st);
