@@ -6,7 +6,8 @@
 // dh_fp28_sqr_vec) accept any two such values with X Y < 2^392 p (about 2500 p^2) and return < 2p; sums and
 // differences are limb-wise with one signed carry pass and no modular reduction (a - b is a + k p - b for a k p
 // above b's bound). So no product slices 12 <-> 14 limbs or subtracts p, and no addition reduces: the point
-// formulas keep their operands below ~50 p. Equality and infinity tests reduce first (f28_zero: one product by 1).
+// formulas keep their operands below ~50 p. Equality tests reduce first (f28_zero: one product by 1); infinity is a
+// flag (j28).
 // Bounds (units of p): dbl (X, Y, Z) <= (48, 50, 2500/Y) -> (26, 18, 4); madd with q < 2 -> (8, 6, 6); add -> (8, 6, 2).
 #pragma once
 #include "fp.hpp"
@@ -147,11 +148,15 @@ DH_DEV f28 f28_from_fp(const fp& x) {
   return f28_mul(a, c);
 }
 
+// Jacobian point with an explicit infinity flag: the subgroup test's points lie on E(Fp), whose order h r is odd
+// (no 2-torsion), so the formulas below only reach infinity through their special cases, which set the flag; a
+// finite point's Z never vanishes (Z3 = 2YZ, 2 Z H, 2 Z1 Z2 H with Y, Z, H != 0), and no product is spent testing it
 struct j28 {
   f28 x, y, z;
+  bool inf;
 };
 
-// dbl-2009-l (a = 0), 2M + 5S. In X <= 48, Y <= 50, Y Z <= 2500 -> out (26, 18, 4); Z = 0 mod p propagates
+// dbl-2009-l (a = 0), 2M + 5S. In X <= 48, Y <= 50, Y Z <= 2500 -> out (26, 18, 4); infinity propagates
 DH_DEV j28 j28_dbl(const j28& p) {
   const f28 a = f28_sqr(p.x);                                          // < 2
   const f28 b = f28_sqr(p.y);                                          // < 2
@@ -165,6 +170,7 @@ DH_DEV j28 j28_dbl(const j28& p) {
   const f28 m = f28_mul(e, f28_sub<26>(d, r.x));                       // E (D + 26p - X3): 6 x 38 -> < 2
   r.y = f28_lin<16>(m, 1, c, -8);                                      // M + 16p - 8C < 18
   r.z = f28_scale(f28_mul(p.y, p.z), 2);                               // < 4
+  r.inf = p.inf;
   return r;
 }
 
@@ -174,12 +180,13 @@ DH_DEV j28 j28_inf() {
   r.y = f28_one();
 #pragma unroll
   for (int i = 0; i < 14; i++) r.z.l[i] = 0;
+  r.inf = true;
   return r;
 }
 
 // madd-2007-bl, q affine (x, y < 2), full special cases as curve.hpp jac_add_aff. In (26, 18, 6) -> out (8, 6, 6)
 DH_DEV j28 j28_madd(const j28& p, const f28& qx, const f28& qy) {
-  if (f28_zero(p.z)) return j28{qx, qy, f28_one()};
+  if (p.inf) return j28{qx, qy, f28_one(), false};
   const f28 z1z1 = f28_sqr(p.z);                                       // < 2
   const f28 u2 = f28_mul(qx, z1z1);                                    // < 2
   const f28 s2 = f28_mul(f28_mul(qy, p.z), z1z1);                      // < 2
@@ -195,6 +202,7 @@ DH_DEV j28 j28_madd(const j28& p, const f28& qx, const f28& qy) {
   const f28 r2 = f28_scale(rr, 2);                                     // < 40
   const f28 v = f28_mul(p.x, i);                                       // 26 x 8 -> < 2
   j28 r;
+  r.inf = false;
   r.x = f28_lin3<6>(f28_sqr(r2), 1, j, -1, v, -2);                    // R^2 + 6p - J - 2V < 8
   const f28 m = f28_mul(r2, f28_sub<8>(v, r.x));                       // 40 x 10 -> < 2
   r.y = f28_lin<4>(m, 1, f28_mul(p.y, j), -2);                         // < 6
@@ -204,8 +212,8 @@ DH_DEV j28 j28_madd(const j28& p, const f28& qx, const f28& qy) {
 
 // add-2007-bl, full special cases as curve.hpp jac_add. In (26, 18, 6) x (26, 18, 6) -> out (8, 6, 2)
 DH_DEV j28 j28_add(const j28& p, const j28& q) {
-  if (f28_zero(p.z)) return q;
-  if (f28_zero(q.z)) return p;
+  if (p.inf) return q;
+  if (q.inf) return p;
   const f28 z1z1 = f28_sqr(p.z), z2z2 = f28_sqr(q.z);                 // < 2
   const f28 u1 = f28_mul(p.x, z2z2), u2 = f28_mul(q.x, z1z1);         // < 2
   const f28 s1 = f28_mul(f28_mul(p.y, q.z), z2z2);                    // < 2
@@ -221,6 +229,7 @@ DH_DEV j28 j28_add(const j28& p, const j28& q) {
   const f28 r2 = f28_scale(rr, 2);                                     // < 8
   const f28 v = f28_mul(u1, i);                                        // < 2
   j28 r;
+  r.inf = false;
   r.x = f28_lin3<6>(f28_sqr(r2), 1, j, -1, v, -2);                    // < 8
   const f28 m = f28_mul(r2, f28_sub<8>(v, r.x));                       // 8 x 10 -> < 2
   r.y = f28_lin<4>(m, 1, f28_mul(s1, j), -2);                          // < 6
@@ -239,7 +248,7 @@ DH_DEV bool g1_in_subgroup28(LD ld) {
   {
     const aff<fp> p = ld();
     const f28 x = f28_from_fp(p.x), y = f28_from_fp(p.y);
-    j28 acc{x, y, f28_one()};
+    j28 acc{x, y, f28_one(), false};
 #pragma unroll 1
     for (int b = 62; b >= 0; b--) {
       acc = j28_dbl(acc);
@@ -253,7 +262,7 @@ DH_DEV bool g1_in_subgroup28(LD ld) {
     acc = j28_dbl(acc);
     if ((cst::U_ABS >> b) & 1) acc = j28_add(acc, t);
   }
-  if (f28_zero(acc.z)) return false;  // phi(P) is finite
+  if (acc.inf) return false;  // phi(P) is finite
   asm volatile("" ::: "memory");      // reload P rather than keep it live through the loop
   const aff<fp> p = ld();
   const f28 bx = f28_from_fp(fp_mul(p.x, fp_c(cst::BETA)));           // phi(P).x < 2

@@ -36,15 +36,15 @@ def from_fp(x): # x is the normal field element
     xr=x*R%p
     return mont(xr, pow(2,400,p))
 def dbl(P):
-    X,Y,Z=P
+    X,Y,Z,fl=P
     a=mont(X,X); b=mont(Y,Y); c=mont(b,b); t=mont(add(X,b),add(X,b))
     d=lin3(8,t,2,a,-2,c,-2); e=scale(a,3); f=mont(e,e)
     x=lin(24,f,1,d,-2); m=mont(e,sub(26,d,x)); y=lin(16,m,1,c,-8); z=scale(mont(Y,Z),2)
-    return (x,y,z)
-def inf(): return (ONE,ONE,0)
+    return (x,y,z,fl)
+def inf(): return (ONE,ONE,0,True)
 def madd(P,qx,qy):
-    X,Y,Z=P
-    if zero(Z): return (qx,qy,ONE)
+    X,Y,Z,fl=P
+    if fl: return (qx,qy,ONE,False)
     z1z1=mont(Z,Z); u2=mont(qx,z1z1); s2=mont(mont(qy,Z),z1z1)
     h=sub(26,u2,X); rr=sub(18,s2,Y)
     if zero(h):
@@ -53,11 +53,11 @@ def madd(P,qx,qy):
     x=lin3(6,mont(r2,r2),1,j,-1,v,-2)
     m=mont(r2,sub(8,v,x)); y=lin(4,m,1,mont(Y,j),-2)
     zs=add(Z,h); z=lin3(4,mont(zs,zs),1,z1z1,-1,hh,-1)
-    return (x,y,z)
+    return (x,y,z,False)
 def jadd(P,Q):
-    X1,Y1,Z1=P; X2,Y2,Z2=Q
-    if zero(Z1): return Q
-    if zero(Z2): return P
+    X1,Y1,Z1,f1=P; X2,Y2,Z2,f2=Q
+    if f1: return Q
+    if f2: return P
     z1z1=mont(Z1,Z1); z2z2=mont(Z2,Z2); u1=mont(X1,z2z2); u2=mont(X2,z1z1)
     s1=mont(mont(Y1,Z2),z2z2); s2=mont(mont(Y2,Z1),z1z1)
     h=sub(2,u2,u1); rr=sub(2,s2,s1)
@@ -67,12 +67,12 @@ def jadd(P,Q):
     x=lin3(6,mont(r2,r2),1,j,-1,v,-2)
     m=mont(r2,sub(8,v,x)); y=lin(4,m,1,mont(s1,j),-2)
     zs=add(Z1,Z2); zz=lin3(4,mont(zs,zs),1,z1z1,-1,z2z2,-1); z=mont(zz,h)
-    return (x,y,z)
+    return (x,y,z,False)
 U=0xd201000000010000
 BETA=0x5f19672fdf76ce51ba69c6076a0f77eaddb3a93be6f89688de17d813620a00022e01fffffffefffe
 def insub(px,py,beta):
     x=from_fp(px); y=from_fp(py)
-    acc=(x,y,ONE)
+    acc=(x,y,ONE,False)
     for b in range(62,-1,-1):
         acc=dbl(acc)
         if (U>>b)&1: acc=madd(acc,x,y)
@@ -80,8 +80,9 @@ def insub(px,py,beta):
     for b in range(62,-1,-1):
         acc=dbl(acc)
         if (U>>b)&1: acc=jadd(acc,t)
-    X,Y,Z=acc
-    if zero(Z): return False
+    X,Y,Z,fl=acc
+    assert fl == zero(Z), "the infinity flag and Z = 0 disagree"
+    if fl: return False
     bx=mont(from_fp(beta),x); z2=mont(Z,Z); z3=mont(z2,Z)
     if not zero(sub(26,mont(bx,z2),X)): return False
     return zero(add(mont(y,z3),Y))
