@@ -156,20 +156,37 @@ struct j28 {
   bool inf;
 };
 
-// dbl-2009-l (a = 0), 2M + 5S. In X <= 48, Y <= 50, Y Z <= 2500 -> out (26, 18, 4); infinity propagates
+// the products inlined (fp_mul28.hpp), for the doubling that makes up the subgroup test's loops: the compiler
+// allocates its operands freely instead of moving them into the call's fixed registers
+DH_DEV f28 f28_mul_inl(const f28& a, const f28& b) {
+  f28 r;
+  m28::mont_mul(r.l, a.l, b.l);
+  return r;
+}
+DH_DEV f28 f28_sqr_inl(const f28& a) {
+  f28 r;
+  m28::mont_sqr(r.l, a.l);
+  return r;
+}
+
+// dbl-2009-l (a = 0), 2M + 5S. In X <= 48, Y <= 50, Y Z <= 2500 -> out (26, 18, 4); infinity propagates.
+// INL: products inlined (the subgroup test's hot loops) or entered out of line (the rare special cases)
+template <bool INL = false>
 DH_DEV j28 j28_dbl(const j28& p) {
-  const f28 a = f28_sqr(p.x);                                          // < 2
-  const f28 b = f28_sqr(p.y);                                          // < 2
-  const f28 c = f28_sqr(b);                                            // < 2
-  const f28 t = f28_sqr(f28_add(p.x, b));                              // (X + B)^2, X + B < 50
+  auto sq = [](const f28& x) { return INL ? f28_sqr_inl(x) : f28_sqr(x); };
+  auto mu = [](const f28& x, const f28& y) { return INL ? f28_mul_inl(x, y) : f28_mul(x, y); };
+  const f28 a = sq(p.x);                                               // < 2
+  const f28 b = sq(p.y);                                               // < 2
+  const f28 c = sq(b);                                                 // < 2
+  const f28 t = sq(f28_add(p.x, b));                                   // (X + B)^2, X + B < 50
   const f28 d = f28_lin3<8>(t, 2, a, -2, c, -2);                       // D = 2 (T + 4p - A - C) < 12
   const f28 e = f28_scale(a, 3);                                       // E = 3A < 6
-  const f28 f = f28_sqr(e);                                            // < 2
+  const f28 f = sq(e);                                                 // < 2
   j28 r;
   r.x = f28_lin<24>(f, 1, d, -2);                                      // F + 24p - 2D < 26
-  const f28 m = f28_mul(e, f28_sub<26>(d, r.x));                       // E (D + 26p - X3): 6 x 38 -> < 2
+  const f28 m = mu(e, f28_sub<26>(d, r.x));                            // E (D + 26p - X3): 6 x 38 -> < 2
   r.y = f28_lin<16>(m, 1, c, -8);                                      // M + 16p - 8C < 18
-  r.z = f28_scale(f28_mul(p.y, p.z), 2);                               // < 4
+  r.z = f28_scale(mu(p.y, p.z), 2);                                    // < 4
   r.inf = p.inf;
   return r;
 }
@@ -251,7 +268,7 @@ DH_DEV bool g1_in_subgroup28(LD ld) {
     j28 acc{x, y, f28_one(), false};
 #pragma unroll 1
     for (int b = 62; b >= 0; b--) {
-      acc = j28_dbl(acc);
+      acc = j28_dbl<true>(acc);
       if ((cst::U_ABS >> b) & 1) acc = j28_madd(acc, x, y);
     }
     t = acc;  // (26, 18, 4): the last step is a doubling
@@ -259,7 +276,7 @@ DH_DEV bool g1_in_subgroup28(LD ld) {
   j28 acc = t;
 #pragma unroll 1
   for (int b = 62; b >= 0; b--) {
-    acc = j28_dbl(acc);
+    acc = j28_dbl<true>(acc);
     if ((cst::U_ABS >> b) & 1) acc = j28_add(acc, t);
   }
   if (acc.inf) return false;  // phi(P) is finite
