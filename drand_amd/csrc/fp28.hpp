@@ -151,6 +151,27 @@ DH_DEV f28 f28_from_fp(const fp& x) {
 // Jacobian point with an explicit infinity flag: the subgroup test's points lie on E(Fp), whose order h r is odd
 // (no 2-torsion), so the formulas below only reach infinity through their special cases, which set the flag; a
 // finite point's Z never vanishes (Z3 = 2YZ, 2 Z H, 2 Z1 Z2 H with Y, Z, H != 0), and no product is spent testing it
+// 28-bit form (< 2p) -> 12 x 32-bit Montgomery form, canonical: one product with 2^384 mod p
+DH_DEV fp f28_to_fp(const f28& a) {
+  f28 c;
+  const uint32_t k[14] = {0x002fffdu, 0x0900000u, 0xc000276u, 0x000bc40u, 0x8baebf4u, 0x5753c75u, 0x55f4898u,
+                          0x7052574u, 0x7ce5853u, 0x56ec6d7u, 0x71a97a2u, 0xe4935c0u, 0xec3fa80u, 0x0015f65u};
+#pragma unroll
+  for (int i = 0; i < 14; i++) c.l[i] = k[i];
+  const f28 r = f28_mul(a, c);
+  fp o;
+  m28::join(o.v, r.l);
+  m28::final_sub(o.v);
+  return o;
+}
+
+DH_DEV f28 f28_c(const uint32_t* c) {
+  f28 r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = c[i];
+  return r;
+}
+
 struct j28 {
   f28 x, y, z;
   bool inf;

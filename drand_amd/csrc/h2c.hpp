@@ -11,6 +11,7 @@
 #pragma once
 #include "curve.hpp"
 #include "sha256.hpp"
+#include "fp28.hpp"
 
 namespace dh {
 
@@ -74,31 +75,36 @@ DH_DEV swu_out<fp> sswu_g1(const fp& u) {
 // 11-isogeny E1' -> E1 (RFC 9380 E.2) on a Jacobian point of E1' (x = X/Z^2, y = Y/Z^3), Jacobian output,
 // Z' = 0 if a denominator vanishes (the point is in the isogeny's kernel: its image is the identity).
 // Homogeneous Horner in x = X / D with D = Z^2: acc_d = acc_d * X + c_{d-j} * D^j, j = 1..deg.
+// Evaluated on lazily reduced 28-bit limbs (fp28.hpp): the ~120 products skip the 12 <-> 14 limb slicing and the
+// Horner sums skip their reductions (every accumulator stays < 4p, a product input up to ~50p); three conversion
+// products in (X, Y, Z) and three out.
 DH_DEV jac<fp> iso11_jac(const jac<fp>& p) {
   using namespace cst;
-  const fp D = fp_sqr(p.z);
-  fp xn = fp_c(ISO11_XNUM[ISO11_XNUM_LEN - 1]);
-  fp xd = fp_c(ISO11_XDEN[ISO11_XDEN_LEN - 1]);
-  fp yn = fp_c(ISO11_YNUM[ISO11_YNUM_LEN - 1]);
-  fp yd = fp_c(ISO11_YDEN[ISO11_YDEN_LEN - 1]);
-  fp zp = D;
+  const f28 X = f28_from_fp(p.x), Zp = f28_from_fp(p.z);
+  const f28 D = f28_sqr(Zp);                                            // < 2
+  f28 xn = f28_c(ISO11_XNUM_28[ISO11_XNUM_LEN - 1]);
+  f28 xd = f28_c(ISO11_XDEN_28[ISO11_XDEN_LEN - 1]);
+  f28 yn = f28_c(ISO11_YNUM_28[ISO11_YNUM_LEN - 1]);
+  f28 yd = f28_c(ISO11_YDEN_28[ISO11_YDEN_LEN - 1]);
+  f28 zp = D;
 #pragma unroll 1
   for (int j = 1; j < ISO11_YNUM_LEN; j++) {
-    if (j > 1) zp = fp_mul(zp, D);
-    yn = fp_add(fp_mul(yn, p.x), fp_mul(fp_c(ISO11_YNUM[ISO11_YNUM_LEN - 1 - j]), zp));
-    yd = fp_add(fp_mul(yd, p.x), fp_mul(fp_c(ISO11_YDEN[ISO11_YDEN_LEN - 1 - j]), zp));
-    if (j < ISO11_XNUM_LEN) xn = fp_add(fp_mul(xn, p.x), fp_mul(fp_c(ISO11_XNUM[ISO11_XNUM_LEN - 1 - j]), zp));
-    if (j < ISO11_XDEN_LEN) xd = fp_add(fp_mul(xd, p.x), fp_mul(fp_c(ISO11_XDEN[ISO11_XDEN_LEN - 1 - j]), zp));
+    if (j > 1) zp = f28_mul(zp, D);                                     // < 2
+    yn = f28_add(f28_mul(yn, X), f28_mul(f28_c(ISO11_YNUM_28[ISO11_YNUM_LEN - 1 - j]), zp));  // < 4
+    yd = f28_add(f28_mul(yd, X), f28_mul(f28_c(ISO11_YDEN_28[ISO11_YDEN_LEN - 1 - j]), zp));
+    if (j < ISO11_XNUM_LEN) xn = f28_add(f28_mul(xn, X), f28_mul(f28_c(ISO11_XNUM_28[ISO11_XNUM_LEN - 1 - j]), zp));
+    if (j < ISO11_XDEN_LEN) xd = f28_add(f28_mul(xd, X), f28_mul(f28_c(ISO11_XDEN_28[ISO11_XDEN_LEN - 1 - j]), zp));
   }
   // x' = xn / (xd D) = Nx / a, y' = (Y / Z^3) yn / yd = Ny / (Z^3 yd)   (deg xn = deg xd + 1, deg yn = deg yd)
   // Z' = a yd Z^3, X' = Nx yd Z^3 Z', Y' = Y yn a Z'^2
-  const fp a = fp_mul(xd, D);
-  const fp z3 = fp_mul(D, p.z);
-  const fp ydz3 = fp_mul(yd, z3);
+  const f28 a = f28_mul(xd, D);
+  const f28 z3 = f28_mul(D, Zp);
+  const f28 ydz3 = f28_mul(yd, z3);
+  const f28 rz = f28_mul(a, ydz3);
   jac<fp> r;
-  r.z = fp_mul(a, ydz3);
-  r.x = fp_mul(fp_mul(xn, ydz3), r.z);
-  r.y = fp_mul(fp_mul(fp_mul(p.y, yn), a), fp_sqr(r.z));
+  r.z = f28_to_fp(rz);
+  r.x = f28_to_fp(f28_mul(f28_mul(xn, ydz3), rz));
+  r.y = f28_to_fp(f28_mul(f28_mul(f28_mul(f28_from_fp(p.y), yn), a), f28_sqr(rz)));
   return r;
 }
 

@@ -148,6 +148,11 @@ def c_fp(x):
     return "{" + ", ".join("0x%08xu" % v for v in limbs(mont(x))) + "}"
 
 
+def c_fp28(x):
+    m = (x % P) * (1 << 392) % P
+    return "{" + ", ".join("0x%07xu" % ((m >> (28 * i)) & 0xFFFFFFF) for i in range(14)) + "}"
+
+
 def c_fp2(a):
     return "{" + c_fp(a[0]) + ", " + c_fp(a[1]) + "}"
 
@@ -334,6 +339,8 @@ def main():
         cs = [int(t, 16) for t in txt.split()]
         w("constexpr int %s_LEN = %d;" % (name, len(cs)))
         w("__device__ __constant__ uint32_t %s[%d][12] = {%s};" % (name, len(cs), ", ".join(c_fp(c) for c in cs)))
+        # the same coefficients for the lazily reduced 28-bit evaluation (fp28.hpp: c 2^392 mod p, 14 x 28-bit limbs)
+        w("__device__ __constant__ uint32_t %s_28[%d][14] = {%s};" % (name, len(cs), ", ".join(c_fp28(c) for c in cs)))
     for name, cs in (("ISO3_XNUM", ISO3_XNUM), ("ISO3_XDEN", ISO3_XDEN), ("ISO3_YNUM", ISO3_YNUM),
                      ("ISO3_YDEN", ISO3_YDEN)):
         w("constexpr int %s_LEN = %d;" % (name, len(cs)))
