@@ -295,8 +295,10 @@ def main():
     if dom:
         avg_s = kern[dom]["total_ms"] / kern[dom]["count"] / 1000.0
         achieved = units[dom] * wm["mul32_per_M"] * n / avg_s
-        traffic = None  # HBM bytes per launch from the committed PMC passes (bench/profile.sh, pmc_summary.py)
-        pmc = os.path.join(ROOT, "profiles", wm.get("pmc_file", "pmc_r02.json"))
+        # HBM bytes per launch from the committed PMC passes (bench/profile.sh, pmc_summary.py); the summary is kept
+        # under bench/ (profiles/ does not travel to the GPU box) with the same file in profiles/
+        traffic = None
+        pmc = os.path.join(ROOT, wm.get("pmc_file", "bench/pmc_r02h.json"))
         if os.path.exists(pmc):
             per_round = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_round")
             traffic = round(per_round * n) if per_round is not None else None
