@@ -3,7 +3,7 @@
 Every value is the integer the device holds (14 normalised 28-bit limbs, Montgomery radix R' = 2^392). mont() is
 fp_mul28.hpp mont_mul (exact integer (a b + m p) / R') and asserts the < 2p output bound the formulas rely on; lin()
 is f28_lin and asserts the result stays in [0, 2^392); the formulas follow fp28.hpp line by line (j28_dbl, j28_madd,
-j28_add, g1_in_subgroup28). Test infrastructure only.
+j28_add, g1_in_subgroup28) and the 11-isogeny of the G1 hash (h2c.hpp iso11_jac). Test infrastructure only.
 """
 p=0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
 r=0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
@@ -86,3 +86,22 @@ def insub(px,py,beta):
     bx=mont(from_fp(beta),x); z2=mont(Z,Z); z3=mont(z2,Z)
     if not zero(sub(26,mont(bx,z2),X)): return False
     return zero(add(mont(y,z3),Y))
+
+def to_fp(a):  # f28_to_fp: one product by 2^384 mod p, then the final subtraction -> canonical x R mod p
+    o=mont(a, R%p)
+    return o-p if o>=p else o
+def iso11(X32,Y32,Z32,xnum,xden,ynum,yden):
+    """iso11_jac on a Jacobian point given in 12 x 32-bit Montgomery form (values x R mod p, canonical); coefficient
+    lists low degree first as in RFC 9380 (normal field elements); returns (X', Y', Z') in the same form."""
+    c=lambda v: v*RP%p
+    f=lambda v: mont(v, pow(2,400,p))  # f28_from_fp on the stored value
+    X=f(X32); Zp=f(Z32); D=mont(Zp,Zp)
+    xn=c(xnum[-1]); xd=c(xden[-1]); yn=c(ynum[-1]); yd=c(yden[-1]); zp=D
+    for j in range(1,len(ynum)):
+        if j>1: zp=mont(zp,D)
+        yn=add(mont(yn,X),mont(c(ynum[-1-j]),zp))
+        yd=add(mont(yd,X),mont(c(yden[-1-j]),zp))
+        if j<len(xnum): xn=add(mont(xn,X),mont(c(xnum[-1-j]),zp))
+        if j<len(xden): xd=add(mont(xd,X),mont(c(xden[-1-j]),zp))
+    a=mont(xd,D); z3=mont(D,Zp); ydz3=mont(yd,z3); rz=mont(a,ydz3)
+    return (to_fp(mont(mont(xn,ydz3),rz)), to_fp(mont(mont(mont(f(Y32),yn),a),mont(rz,rz))), to_fp(rz))
