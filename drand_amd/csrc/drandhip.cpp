@@ -634,6 +634,16 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   const std::vector<size_t>& fixed = fixed_ladder();
   size_t gsize = n;
   int level = 0;
+  if (mode == VM_BEGIN && n < 2) {
+    // a one-round batch has no level-0 group: it contributes the identity (Z = 0) to the node-wide sums, and
+    // dh_batch_finish gives the round its own leaf check whatever the node check says
+    HIP_TRY(w->outA.ensure(jw * 4));
+    HIP_TRY(w->outB.ensure(jw * 4));
+    HIP_TRY(hipMemsetAsync(w->outA.p, 0, jw * 4, st));
+    HIP_TRY(hipMemsetAsync(w->outB.p, 0, jw * 4, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return DH_OK;
+  }
   while (m > 0 && gsize > 1) {
     gsize = std::min(gsize, m);
     dh::msm_geom g = geom_for(gsize, true);

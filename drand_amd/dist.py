@@ -5,17 +5,33 @@
 * Chained halo: a chained shard's first round needs the STORED signature of round start-1
   (/root/reference/chain/boltdb/trimmed.go:183), which lives in the previous rank's shard. shard_beacons reads it
   from the shared store (host-supplied halo); exchange_halo passes it rank to rank when each rank only holds its
-  own shard (e.g. each streams its range from a different peer).
+  own shard (e.g. each streams its range from a different peer). A missing round start-1 travels as MISSING_HALO,
+  and the next rank reports its first round missing, as the trimmed store's Get would (trimmed.go:183-187).
 * Node-wide check: every rank computes its level-0 RLC sums (A_g, B_g) with dh_batch_begin; one all-gather of
-  those 2 points per rank over RCCL (xGMI), then ONE pairing check of the sums for the whole node
-  (dh_check_partials) and dh_batch_finish: all ranks accept, or each bisects its own shard. No data-path collective
-  besides that (the per-round data never leaves its GPU).
+  those 2 points (plus a status byte) per rank over RCCL (xGMI), then ONE pairing check of the sums for the whole
+  node (dh_check_partials) and dh_batch_finish: all ranks accept, or each bisects its own shard. A rank whose
+  dh_batch_begin failed still takes part in the exchange (identity sums, status 1), so every rank abandons the
+  batch together instead of blocking in the collective. No data-path collective besides that (the per-round data
+  never leaves its GPU).
 * Verdicts: packed bitmaps all-gathered once at the end (gather_verdicts).
-The collectives use torch.distributed: backend "nccl" (= RCCL) on the GPUs, "gloo" in the CPU tests.
+* replay_shard: the sharded CheckPastBeacons (chain/beacon/sync_manager.go:170-235) built from the pieces above.
+The collectives use torch.distributed: backend "nccl" (= RCCL) with device tensors, "gloo" with host tensors
+(the CPU tests, and N ranks rehearsed on one GPU).
 """
 import ctypes
+import hashlib
 
 import numpy as np
+
+PREV_SLOT_MAX = 4096  # as scheme.PREV_SLOT_MAX: longer stored records only come from a corrupted store
+
+
+class _MissingHalo:
+    def __repr__(self):
+        return "MISSING_HALO"
+
+
+MISSING_HALO = _MissingHalo()
 
 
 def shard_rounds(rank, world, n_per_rank, first_round=1):
@@ -60,27 +76,42 @@ def shard_beacons(store, rank, world, first, last):
     return rounds, sigs, prevs, missing
 
 
-def exchange_halo(last_signature, rank, world, group=None, max_len=96):
-    """Rank r receives rank r-1's last stored signature (rank 0 gets None): one all-gather of a fixed-size slot
-    (length + bytes) per rank. Used when each rank holds only its own shard of the chain."""
+def _collective_device(group):
+    """Where the collective's tensors live: the current GPU under nccl (RCCL), the host under gloo."""
     import torch
     import torch.distributed as dist
-    slot = torch.zeros(max_len + 4, dtype=torch.uint8)
-    sig = bytes(last_signature or b"")
-    if len(sig) > max_len:
-        raise ValueError("signature longer than the halo slot")
-    slot[:4] = torch.tensor(list(len(sig).to_bytes(4, "little")), dtype=torch.uint8)
-    if sig:
-        slot[4:4 + len(sig)] = torch.tensor(list(sig), dtype=torch.uint8)
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def exchange_halo(last_signature, rank, world, group=None):
+    """Rank r receives rank r-1's last stored signature (a stored record may have any length): an all-gather of
+    the record lengths, then one of slots that fit the longest, on the device under nccl. `last_signature` is None
+    when this shard's last round is missing from the store: the next rank then gets MISSING_HALO. Rank 0 (and
+    world 1) gets None."""
+    import torch
+    import torch.distributed as dist
     if world == 1:
         return None
+    dev = _collective_device(group)
+    missing = last_signature is None
+    sig = b"" if missing else bytes(last_signature)
+    ln = torch.tensor([-1 if missing else len(sig)], dtype=torch.int64, device=dev)
+    lens = [torch.zeros_like(ln) for _ in range(world)]
+    dist.all_gather(lens, ln, group=group)
+    width = max(1, max(int(x) for x in lens))
+    host = np.zeros(width, dtype=np.uint8)
+    host[:len(sig)] = np.frombuffer(sig, np.uint8)
+    slot = torch.from_numpy(host).to(dev)
     out = [torch.zeros_like(slot) for _ in range(world)]
     dist.all_gather(out, slot, group=group)
     if rank == 0:
         return None
-    prev = out[rank - 1].numpy().tobytes()
-    n = int.from_bytes(prev[:4], "little")
-    return prev[4:4 + n]
+    n = int(lens[rank - 1])
+    if n < 0:
+        return MISSING_HALO
+    return out[rank - 1].cpu().numpy().tobytes()[:n]
 
 
 def pack_bits(verdict):
@@ -127,30 +158,62 @@ def gather_partials(local, world, group=None):
     return out
 
 
+def rank_seed(seed, rank):
+    """A caller-fixed RLC seed made distinct per rank: the scalars are SHA-256(seed || local index), so equal
+    seeds would give every rank the same scalar at the same index, and errors planted at one index on two ranks
+    could cancel in the node-wide sums. 0 stays 0 (fresh CSPRNG seed per call in the library)."""
+    if not seed:
+        return 0
+    h = hashlib.sha256(b"drandhip-rank-seed" + int(seed).to_bytes(8, "little") + int(rank).to_bytes(4, "little"))
+    return int.from_bytes(h.digest()[:8], "little") or 1
+
+
 def verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, partials, world, group=None,
-                      d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=False):
+                      d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=None, rank=None):
     """One batch of this rank's shard under the node-wide check: dh_batch_begin -> all-gather of the (A, B) sums
-    -> dh_check_partials (one pairing check for the whole node) -> dh_batch_finish. `partials` is a uint8 device
-    tensor of dh_partial_bytes(scheme) bytes; with stage_host the exchange goes through host memory (gloo).
-    Returns the node-wide pass flag."""
+    and a status byte -> dh_check_partials (one pairing check for the whole node) -> dh_batch_finish. `partials` is
+    a uint8 device tensor of dh_partial_bytes(scheme) bytes; the exchange runs on the device under nccl and through
+    host memory otherwise (stage_host=None picks by backend). Returns the node-wide pass flag. If any rank's
+    dh_batch_begin failed, every rank abandons the batch and raises."""
     import torch
+    import torch.distributed as dist
     from . import _lib
+
+    if rank is None:
+        rank = dist.get_rank(group) if world > 1 else 0
 
     def ptr(t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
     b = ctypes.c_void_p()
     rc = lib.dh_batch_begin(scheme.id, pk, len(pk), ptr(d_rounds), ptr(d_sigs), scheme.sig_len, ptr(d_prevs),
-                            prev_stride, ptr(d_prev_lens), n, ptr(d_verdict), ptr(d_rand), seed, None,
+                            prev_stride, ptr(d_prev_lens), n, ptr(d_verdict), ptr(d_rand), rank_seed(seed, rank), None,
                             ctypes.byref(b), ptr(partials))
-    if rc != 0:
-        raise RuntimeError("dh_batch_begin: %s" % _lib.last_error())
+    err = None if rc == 0 else "rank %d: dh_batch_begin: %s" % (rank, _lib.last_error())
+    if world == 1:
+        if err:
+            raise RuntimeError(err)
+        allp = partials
+    else:
+        pb = partials.numel()
+        if stage_host is None:
+            stage_host = not dist.get_backend(group) == "nccl"
+        dev = torch.device("cpu") if stage_host else partials.device
+        slot = torch.zeros(pb + 4, dtype=torch.uint8, device=dev)
+        if err is None:
+            slot[:pb] = partials.to(dev)  # identity (zeros) otherwise
+        slot[pb] = 0 if err is None else 1
+        gathered = gather_partials(slot, world, group).view(world, pb + 4)
+        status = gathered[:, pb].cpu().numpy()
+        if status.any():
+            if err is None:
+                lib.dh_batch_finish(b, -1, None)
+            bad = [int(r) for r in np.flatnonzero(status)]
+            raise RuntimeError(err or "node batch abandoned: dh_batch_begin failed on rank(s) %s" % bad)
+        allp = gathered[:, :pb].contiguous().to(partials.device)
     try:
-        if stage_host:
-            allp = gather_partials(partials.cpu(), world, group).to(partials.device)
-        else:
-            allp = gather_partials(partials, world, group)
-        torch.cuda.current_stream(partials.device).synchronize()  # the library reads it from its own streams
+        if allp.is_cuda:
+            torch.cuda.current_stream(allp.device).synchronize()  # the library reads it from its own streams
         ok = ctypes.c_int(0)
         rc = lib.dh_check_partials(scheme.id, pk, len(pk), ptr(allp), world, ctypes.byref(ok))
         if rc != 0:
@@ -162,3 +225,86 @@ def verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, p
     if rc != 0:
         raise RuntimeError("dh_batch_finish: %s" % _lib.last_error())
     return bool(ok.value)
+
+
+def replay_shard(lib, scheme, pk, first, last, sig_of, rank, world, group=None, prev_of_first=None, seed=0,
+                 device=None):
+    """This rank's part of a sharded chain replay (CheckPastBeacons' verification over the node,
+    /root/reference/chain/beacon/sync_manager.go:191-225, sharded as SURVEY.md §8e): rounds first..last are split
+    with shard_range, and `sig_of` maps each round of this rank's range to its stored signature (a round absent
+    from it is missing from the store). Chained: the previous signature of round k is the stored signature of
+    k-1 (chain/boltdb/trimmed.go:183); the one before this rank's first round comes from the previous rank
+    (exchange_halo), or from `prev_of_first` on rank 0 (the stored record of round first-1: the genesis seed when
+    first = 1). A round is faulty when it is missing, its previous record is missing (chained), or it fails
+    VerifyBeacon. The present rounds are verified in one batch under the node-wide check (verify_node_batch) and
+    the ranks' verdicts all-gathered: every rank returns the whole node's faulty rounds, ascending."""
+    import torch
+    from .sync import NoBeaconStored  # noqa: F401  (the store error this mirrors)
+
+    lo, hi = shard_range(rank, world, last - first + 1)
+    lo, hi = first + lo, first + hi
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    halo = None
+    if scheme.chained and world > 1:
+        # only trailing ranks can be empty (shard_range gives the extra rounds to the lower ranks): they need no halo
+        halo = exchange_halo(sig_of.get(hi - 1) if hi > lo else None, rank, world, group)
+    prev_first = prev_of_first if rank == 0 else halo
+    if prev_first is MISSING_HALO:
+        prev_first = None
+    ok_range = np.zeros(hi - lo, dtype=np.uint8)
+    idx, prevs = [], []
+    for k, r in enumerate(range(lo, hi)):
+        sig = sig_of.get(r)
+        if sig is None:
+            continue
+        if scheme.chained:
+            p = prev_first if r == lo else sig_of.get(r - 1)
+            if p is None:
+                continue  # Get fails: previous record missing (trimmed.go:183-187)
+            prevs.append(bytes(p))
+        idx.append(k)
+    n = len(idx)
+    sigs = np.zeros((max(n, 1), scheme.sig_len), dtype=np.uint8)
+    bad_len = np.zeros(max(n, 1), dtype=bool)
+    for j, k in enumerate(idx):
+        s = bytes(sig_of[lo + k])
+        if len(s) == scheme.sig_len:
+            sigs[j] = np.frombuffer(s, np.uint8)
+        else:
+            bad_len[j] = True  # an all-zero record never decodes: rejected like kyber's length check
+    rounds = np.array([lo + k for k in idx] or [0], dtype=np.uint64)
+    d_prevs = d_plen = None
+    stride = 0
+    oversize = np.zeros(max(n, 1), dtype=bool)
+    if scheme.chained and n:
+        lens = np.array([len(p) for p in prevs], dtype=np.uint32)
+        oversize[:n] = lens > PREV_SLOT_MAX
+        stride = max(96, (int(min(lens.max(), PREV_SLOT_MAX)) + 3) // 4 * 4)
+        pcol = np.zeros((n, stride), dtype=np.uint8)
+        for j, p in enumerate(prevs):
+            if not oversize[j]:
+                pcol[j, :len(p)] = np.frombuffer(p, np.uint8)
+        lens[oversize[:n]] = 0
+        d_prevs = torch.from_numpy(pcol).to(device)
+        d_plen = torch.from_numpy(lens.view(np.int32)).to(device)
+    d_rounds = torch.from_numpy(rounds.view(np.int64)).to(device)
+    d_sigs = torch.from_numpy(sigs).to(device)
+    d_verdict = torch.zeros(max(n, 1), dtype=torch.uint8, device=device)
+    partials = torch.zeros(lib.dh_partial_bytes(scheme.id), dtype=torch.uint8, device=device)
+    verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, None, partials, world, group,
+                      d_prevs=d_prevs, prev_stride=stride, d_prev_lens=d_plen, seed=seed, rank=rank)
+    v = d_verdict.cpu().numpy()[:n].astype(bool) & ~bad_len[:n]
+    if oversize[:n].any():  # previous records beyond the slot: host digest + device pairing check (scheme path)
+        j = np.flatnonzero(oversize[:n])
+        v[j], _ = scheme.verify_beacons(pk, rounds[j], sigs[j], [prevs[i] for i in j], seed=seed,
+                                        want_randomness=False)
+        v[j] &= ~bad_len[j]
+    ok_range[np.array(idx, dtype=np.int64)] = v.astype(np.uint8)
+    bits = pack_bits(torch.from_numpy(ok_range).to(_collective_device(group) if world > 1 else torch.device("cpu")))
+    faulty = []
+    for r_, b_ in enumerate(gather_verdicts(bits, world, group)):
+        a, z = shard_range(r_, world, last - first + 1)
+        got = np.unpackbits(b_.cpu().numpy())[:z - a]
+        faulty += [first + a + int(i) for i in np.flatnonzero(got == 0)]
+    return faulty

@@ -14,8 +14,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from drand_amd.dist import (exchange_halo, gather_partials, gather_verdicts, pack_bits, shard_beacons, shard_range,
-                            shard_rounds, strong_shard)
+from drand_amd.dist import (MISSING_HALO, exchange_halo, gather_partials, gather_verdicts, pack_bits, rank_seed,
+                            shard_beacons, shard_range, shard_rounds, strong_shard, verify_node_batch)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
@@ -41,6 +41,11 @@ def _store_with_boundary_fault(boundary):
     return st, bytes.fromhex(c["pk"]), c["rounds"][-1]
 
 
+def sigs_prev_rank_last(st, rank, world, last):
+    lo, _ = shard_range(rank, world, last)
+    return st.get(lo).signature  # the last round of rank-1 is round lo (rounds start at 1)
+
+
 def _worker(rank, world, port, boundary, q):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as orc
@@ -51,6 +56,10 @@ def _worker(rank, world, port, boundary, q):
     rounds, sigs, prevs, missing = shard_beacons(st, rank, world, 1, last)
     halo = exchange_halo(sigs[-1] if sigs else b"", rank, world)  # rank r-1's last stored signature
     halo_ok = rank == 0 or halo == prevs[0] == st.get(rounds[0] - 1).signature
+    # a shard whose last round is missing from the store hands the next rank MISSING_HALO (trimmed.go:183-187)
+    gone = exchange_halo(None if rank == 0 else sigs[-1], rank, world)
+    halo_ok = halo_ok and gone is (None if rank == 0 else MISSING_HALO if rank == 1 else gone)
+    halo_ok = halo_ok and (rank < 2 or gone == sigs_prev_rank_last(st, rank, world, last))
     verdict = torch.tensor([orc.verify_beacon(CHAINED, pk, r, s, p) for r, s, p in zip(rounds, sigs, prevs)],
                            dtype=torch.uint8)
     parts = gather_verdicts(pack_bits(verdict), world)
@@ -111,3 +120,80 @@ def test_shards_partition_rounds():
 def test_pack_bits_matches_numpy():
     v = (np.arange(29) % 3 == 0).astype(np.uint8)
     assert np.array_equal(pack_bits(torch.from_numpy(v)).numpy(), np.packbits(v))
+
+
+class _FakeLib:
+    """The three node-check entry points of libdrandhip, on the host: dh_batch_begin writes rank-specific partial
+    bytes (or fails on `fail_rank`), dh_check_partials records what the all-gather delivered."""
+
+    def __init__(self, rank, fail_rank, pb):
+        self.rank, self.fail_rank, self.pb = rank, fail_rank, pb
+        self.seed, self.seen, self.finished = None, None, []
+
+    def dh_batch_begin(self, sid, pk, pklen, r, s, sl, p, ps, pl, n, v, rnd, seed, stream, bref, parts):
+        import ctypes
+        self.seed = seed
+        if self.rank == self.fail_rank:
+            return -2
+        ctypes.memmove(parts.value, bytes([self.rank + 1]) * self.pb, self.pb)
+        bref._obj.value = 1000 + self.rank
+        return 0
+
+    def dh_check_partials(self, sid, pk, pklen, allp, k, okref):
+        import ctypes
+        self.seen = ctypes.string_at(allp.value, k * self.pb)
+        okref._obj.value = 1
+        return 0
+
+    def dh_batch_finish(self, b, ok, st):
+        self.finished.append(ok)
+        return 0
+
+
+def _node_worker(rank, world, port, fail_rank, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from drand_amd.scheme import scheme_from_name
+    s = scheme_from_name("pedersen-bls-unchained")
+    pb = 2 * 72 * 4
+    lib = _FakeLib(rank, fail_rank, pb)
+    parts = torch.zeros(pb, dtype=torch.uint8)
+    out = {"rank": rank}
+    try:
+        out["pass"] = verify_node_batch(lib, s, b"k" * 48, None, None, 10, None, None, parts, world, seed=5)
+    except RuntimeError as e:
+        out["error"] = str(e)
+    out.update(seed=lib.seed, seen=lib.seen, finished=lib.finished)
+    q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [None, 1])
+def test_node_batch_protocol_gloo(fail_rank):
+    """verify_node_batch's collective protocol at world 3 over gloo (library entry points faked on the host): the
+    partial sums arrive in rank order at every rank, each rank's RLC seed is distinct (rank_seed), and when
+    dh_batch_begin fails on one rank every rank raises instead of blocking in the all-gather, the ranks that began
+    abandoning their batch (dh_batch_finish(b, -1))."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_node_worker, args=(r, world, port, fail_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in range(world)), key=lambda m: m["rank"])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len({m["seed"] for m in res}) == world and res[0]["seed"] == rank_seed(5, 0) != 5
+    pb = 2 * 72 * 4
+    if fail_rank is None:
+        assert all(m["pass"] is True and m["finished"] == [1] for m in res)
+        assert all(m["seen"] == b"".join(bytes([r + 1]) * pb for r in range(world)) for m in res)
+    else:
+        assert all("error" in m and m["seen"] is None for m in res)
+        assert "dh_batch_begin" in res[fail_rank]["error"] and "rank(s) [1]" in res[0]["error"]
+        assert [m["finished"] for m in res] == [[-1], [], [-1]]
+    assert rank_seed(0, 3) == 0

@@ -351,6 +351,7 @@ def test_sync_from_stream_device(dh):
             for r, x, p in zip(c["rounds"], c["sigs"], c["prevs"])]
     q = queue.Queue()
     st = TrimmedMemStore(True)
+    st.put(0, bytes.fromhex(c["prevs"][0]))  # the genesis record: tryNode starts from the store's Last()
     out = {}
     th = threading.Thread(target=lambda: out.update(res=sync_from_stream(q, s, pk, st, up_to=20, window=500,
                                                                          idle=0.05, max_delay=0.5)))
@@ -358,9 +359,9 @@ def test_sync_from_stream_device(dh):
     for p in pkts[:5]:
         q.put(p)
     deadline = time.time() + 60
-    while st.len() < 5 and time.time() < deadline:  # the live follow stores them with the window far from full
+    while st.len() < 6 and time.time() < deadline:  # the live follow stores them with the window far from full
         time.sleep(0.02)
-    assert st.len() == 5
+    assert st.len() == 6
     for p in pkts[5:]:
         q.put(p)
     q.put(END)
@@ -373,7 +374,9 @@ def test_sync_from_stream_device(dh):
     for p in bad:
         q2.put(p)
     q2.put(END)
-    done, stored = sync_from_stream(q2, s, pk, TrimmedMemStore(True), up_to=24, window=8)
+    st2 = TrimmedMemStore(True)
+    st2.put(0, bytes.fromhex(c["prevs"][0]))
+    done, stored = sync_from_stream(q2, s, pk, st2, up_to=24, window=8)
     assert not done and stored == list(range(1, 13))
 
 

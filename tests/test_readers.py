@@ -170,18 +170,25 @@ def test_stream_sync_windows(oracle):
     pk = bytes.fromhex(c["pk"])
     pk_packets = [{"round": r, "signature": bytes.fromhex(x), "previous_signature": b""}
                   for r, x in zip(c["rounds"], c["sigs"])]
-    st = TrimmedMemStore(False)
+
+    def genesis_store():
+        st = TrimmedMemStore(False)
+        st.put(0, b"genesis seed")  # a chain store always holds the genesis beacon (tryNode starts from Last())
+        return st
+
+    st = genesis_store()
     done, stored = sync_from_stream(pk_packets, s, pk, st, up_to=20, window=6)
     assert done and stored == list(range(1, 21))
     bad = [dict(p) for p in pk_packets]
     bad[9]["signature"] = bad[10]["signature"]  # round 10 invalid: rounds 1..9 stored, then the peer is dropped
-    st = TrimmedMemStore(False)
-    done, stored = sync_from_stream(bad, s, pk, st, up_to=24, window=4)
+    done, stored = sync_from_stream(bad, s, pk, genesis_store(), up_to=24, window=4)
     assert not done and stored == list(range(1, 10))
     wrong_id = [dict(p) for p in pk_packets]
     wrong_id[5]["beacon_id"] = "other"
-    done, stored = sync_from_stream(wrong_id, s, pk, TrimmedMemStore(False), up_to=24, window=4)
+    done, stored = sync_from_stream(wrong_id, s, pk, genesis_store(), up_to=24, window=4)
     assert not done and stored == list(range(1, 6))
+    # an empty store has no Last(): tryNode gives up before asking the peer (sync_manager.go:338-342)
+    assert sync_from_stream(pk_packets, s, pk, TrimmedMemStore(False), up_to=20) == (False, [])
 
 
 def _serial_relay_s3(scheme, pk, get, begin, end):
