@@ -11,7 +11,8 @@ applied blanket: each kernel reports the raw value and the doubled one, and whic
 pattern (the per-round prep kernels read 16-B-per-lane records: doubled; the MSM bucket pass gathers scattered
 points: raw). Per-kernel values are summed over launches and divided by the rounds one launch processes, so
 bench.py can report the traffic of a launch at any batch size (x rounds).
-The VALU-busy pass: SQ_ACTIVE_INST_VALU (quad-cycles in which a wave issued VALU work, summed over waves) over
+Counters are averaged per dispatch (a kernel that also runs while the bench signs its chain, as the G2 hash kernels
+do, is not double counted). The VALU-busy pass: SQ_ACTIVE_INST_VALU (quad-cycles in which a wave issued VALU work, summed over waves) over
 SQ_WAVE_CYCLES (quad-cycles of wave lifetime, summed over waves) = VALU-active share of a wave's life;
 SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES = issue stalls (dependency / pipe), SQ_WAIT_ANY / SQ_WAVE_CYCLES = parked on
 s_waitcnt (memory); GRBM_GUI_ACTIVE / 8 XCDs / duration = effective clock.
@@ -46,10 +47,11 @@ def load(d):
     n = collections.Counter()
     seen = set()
     for name, cname, val, scratch, vgpr, dur in rows(d):
-        m = re.match(r"(?:void )?dh::(k_\w+)(<dh::(fp2?)(?:, (true|false))?>)?", name)
+        m = re.match(r"(?:void )?dh::(k_\w+)(?:<dh::(fp2?)(?:, (true|false))?>|<(true|false)>)?", name)
         if not m:
             continue
-        key = m.group(1) + ("<%s>" % m.group(3) if m.group(3) else "")
+        targs = [x for x in (m.group(2), m.group(3), m.group(4)) if x]
+        key = m.group(1) + ("<%s>" % ", ".join(targs) if targs else "")
         agg[key][cname] += val
         agg[key]["_scratch_per_lane"] = scratch
         agg[key]["_vgpr"] = vgpr
@@ -70,15 +72,20 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--note", default="")
     a = ap.parse_args()
-    f, _ = load(a.fetch)
-    w, _ = load(a.write)
-    sq = load(a.sq)[0] if a.sq else {}
+    f, fn = load(a.fetch)
+    w, wn = load(a.write)
+    sq, sqn = load(a.sq) if a.sq else ({}, {})
     busy = load(a.busy)[0] if a.busy else {}
     out = {"_meta": {"rounds_per_launch": a.rounds, "units": "bytes per round; FETCH_SIZE KiB x1024 (raw, and x2 "
                      "for streaming-read kernels), WRITE_SIZE KiB x1024", "note": a.note}}
+    nd = {}  # dispatches per kernel: the same kernel may run more than once (e.g. the G2 hash kernels also sign)
+    for agg, cnt in ((f, fn), (w, wn)):
+        for (k, c), v in cnt.items():
+            nd[k] = max(nd.get(k, 1), v)
     for k in sorted(set(f) | set(w)):
-        fr = f.get(k, {}).get("FETCH_SIZE", 0.0) * 1024
-        wb = w.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
+        d = float(nd.get(k, 1))
+        fr = f.get(k, {}).get("FETCH_SIZE", 0.0) * 1024 / d
+        wb = w.get(k, {}).get("WRITE_SIZE", 0.0) * 1024 / d
         streaming = k.startswith("k_prep") or k.startswith("k_h2f") or k.startswith("k_sswu") or k.startswith("k_add_iso")
         fb = fr * 2 if streaming else fr
         e = {"fetch_bytes_per_round_raw": round(fr / a.rounds, 2), "fetch_correction": "x2" if streaming else "none",
@@ -88,9 +95,11 @@ def main():
              "vgprs": int(f.get(k, {}).get("_vgpr", 0))}
         if k in sq:
             s = sq[k]
-            e["valu_insts_per_round"] = round(s.get("SQ_INSTS_VALU", 0) * 64 / a.rounds, 1)  # per lane = per round
+            ds = float(max(1, sqn.get((k, "SQ_INSTS_VALU"), 1)))
+            e["dispatches"] = int(ds)
+            e["valu_insts_per_round"] = round(s.get("SQ_INSTS_VALU", 0) * 64 / a.rounds / ds, 1)  # per lane = per round
             e["salu_insts_per_wave"] = round(s.get("SQ_INSTS_SALU", 0) / max(1.0, s.get("SQ_WAVES", 1)), 1)
-            e["flat_insts_per_round"] = round(s.get("SQ_INSTS_FLAT", 0) * 64 / a.rounds, 1)
+            e["flat_insts_per_round"] = round(s.get("SQ_INSTS_FLAT", 0) * 64 / a.rounds / ds, 1)
         if k in busy:
             b = busy[k]
             wc = max(1.0, b.get("SQ_WAVE_CYCLES", 0))

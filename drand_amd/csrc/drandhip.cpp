@@ -92,6 +92,8 @@ struct worker {
   bool busy = false;
   // per-round state
   dbuf status, sig_aff, q_pts, scal, entries, verdict_tmp, rand_tmp, h2c_tmp;
+  // the MSM's 28-bit points (launch_msm_prep28, G1): sigma and its phi image (32 words each), hash points (48 words)
+  dbuf s28, q28;
   // host-API staging
   dbuf in_rounds, in_sigs, in_prevs, in_prev_lens, out_verdict, out_rand;
   // key
@@ -113,7 +115,7 @@ struct worker {
   uint8_t cached_key_ok = 0;
   std::vector<uint32_t> h_entries, h_next;
   void release_all() {
-    dbuf* all[] = {&status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &h2c_tmp, &in_rounds, &in_sigs,
+    dbuf* all[] = {&s28, &q28, &status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &h2c_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
@@ -330,32 +332,49 @@ constexpr size_t JAC_WORDS_G1 = 36, JAC_WORDS_G2 = 72;
 struct prof_entry {
   uint64_t count = 0;
   double ms = 0;
+  unsigned long long prods = 0;  // field products executed (counting build only)
 };
 struct profiler {
   std::mutex mu;
   std::atomic<bool> on{false};  // read on every launch without the lock
   std::vector<std::pair<std::string, prof_entry>> table;
-  void add(const char* name, float ms) {
+  void add(const char* name, float ms, unsigned long long prods = 0) {
     std::lock_guard<std::mutex> lk(mu);
     for (auto& e : table)
       if (e.first == name) {
         e.second.count++;
         e.second.ms += ms;
+        e.second.prods += prods;
         return;
       }
     prof_entry pe;
     pe.count = 1;
     pe.ms = ms;
+    pe.prods = prods;
     table.emplace_back(name, pe);
   }
 };
 profiler g_prof;
 
-// records a launch bracketed by events when profiling is on; resolved after the stream syncs
+#ifdef DH_COUNT_PRODUCTS
+// counting build: products executed by every translation unit's kernels since the last take
+static unsigned long long count_take_all() {
+  unsigned long long t = 0, v = 0;
+  hipError_t (*take[])(unsigned long long*) = {dh::count_take_prep, dh::count_take_msm, dh::count_take_check,
+                                               dh::count_take_sign, dh::count_take_recover, dh::count_take_vm};
+  for (auto f : take)
+    if (f(&v) == hipSuccess) t += v;
+  return t;
+}
+#endif
+
+// records a launch bracketed by events when profiling is on; resolved after the stream syncs. The counting build
+// also synchronises after each launch and attributes the products executed to it (one batch at a time).
 struct timed_launches {
   struct rec {
     const char* name;
     hipEvent_t a, b;
+    unsigned long long prods;
   };
   std::vector<rec> recs;
   hipStream_t st;
@@ -363,19 +382,28 @@ struct timed_launches {
   template <class F>
   hipError_t run(const char* name, F&& f) {
     if (!g_prof.on.load(std::memory_order_relaxed)) return f();
-    rec r{name, nullptr, nullptr};
+    rec r{name, nullptr, nullptr, 0};
     (void)hipEventCreate(&r.a);
     (void)hipEventCreate(&r.b);
+#ifdef DH_COUNT_PRODUCTS
+    (void)hipDeviceSynchronize();
+    (void)count_take_all();
+#endif
     (void)hipEventRecord(r.a, st);
     hipError_t e = f();
     (void)hipEventRecord(r.b, st);
+#ifdef DH_COUNT_PRODUCTS
+    (void)hipDeviceSynchronize();
+    r.prods = count_take_all();
+#endif
     recs.push_back(r);
     return e;
   }
   void resolve() {
     for (auto& r : recs) {
       float ms = 0;
-      if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) g_prof.add(r.name, ms);
+      if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess)
+        g_prof.add(r.name, ms, r.prods);
       (void)hipEventDestroy(r.a);
       (void)hipEventDestroy(r.b);
     }
@@ -533,6 +561,9 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (n >= 0x40000000u) return fail(DH_EINVAL, "batch too large");
   const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
   const size_t aw = jw * 2 / 3;
+  // G1: the MSM runs on lazily reduced 28-bit points (k_msm.hip MSM28), whose workspace points take 48 words
+  const bool msm28 = !g2;
+  const size_t wsw = msm28 ? 48 : jw;
 
   timed_launches T(st);
   bool presorted = false;  // level-0 sorted lists already built on the tail stream
@@ -577,7 +608,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
       HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, ts));
       g0 = geom_for(n, true);
       g0.half_stride = (uint32_t)n;
-      rc = msm_workspace(w, g0, n, 1, jw, ws0);
+      rc = msm_workspace(w, g0, n, 1, wsw, ws0);
       if (rc) return rc;
       HIP_TRY(dh::launch_msm_sort(g0, w->entries.as<uint32_t>(), nullptr, nullptr, n, 1, w->scal.as<uint4>(), ws0, ts));
     }
@@ -597,7 +628,14 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
       HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
       HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), 1, st));
     }
-    HIP_TRY(dh::launch_endo(g2, n, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(), st));
+    if (msm28) {
+      HIP_TRY(w->s28.ensure(2 * n * 32 * 4));
+      HIP_TRY(w->q28.ensure(2 * n * 48 * 4));
+      HIP_TRY(dh::launch_msm_prep28(g2, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
+                                    w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), st));
+    } else {
+      HIP_TRY(dh::launch_endo(g2, n, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(), st));
+    }
     HIP_TRY(hipMemsetAsync(d_verdict, 0, n, st));
     if (gate) {
       HIP_TRY(hipEventRecord(gate->done, st));
@@ -654,12 +692,16 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     if (pre) {
       ws = ws0;
     } else {
-      const int rc = msm_workspace(w, g, m, ngroups, jw, ws);
+      const int rc = msm_workspace(w, g, m, ngroups, wsw, ws);
       if (rc) return rc;
     }
     if (!(level == 0 && mode >= VM_FINISH)) {  // a resumed batch has its level-0 sums from dh_batch_begin
       // every level skips the rounds whose status is not DEC_OK (their scalars are nonzero after a presort)
       HIP_TRY(T.run(msm_names[std::min(level, 7)], [&] {
+        if (msm28)
+          return dh::launch_msm28(g2, pre ? g0 : g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(),
+                                  w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
+                                  w->outB.as<uint32_t>(), st, w->status.as<uint8_t>(), pre);
         return dh::launch_msm(g2, pre ? g0 : g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(),
                               w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
                               w->outB.as<uint32_t>(), st, w->status.as<uint8_t>(), pre);
@@ -1574,8 +1616,8 @@ int dh_profile_read(char* buf, size_t cap) {
   bool first = true;
   for (auto& e : g_prof.table) {
     char tmp[256];
-    snprintf(tmp, sizeof tmp, "%s\"%s\": {\"count\": %llu, \"total_ms\": %.6f}", first ? "" : ", ", e.first.c_str(),
-             (unsigned long long)e.second.count, e.second.ms);
+    snprintf(tmp, sizeof tmp, "%s\"%s\": {\"count\": %llu, \"total_ms\": %.6f, \"products\": %llu}", first ? "" : ", ",
+             e.first.c_str(), (unsigned long long)e.second.count, e.second.ms, e.second.prods);
     out += tmp;
     first = false;
   }

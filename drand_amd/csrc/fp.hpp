@@ -256,6 +256,7 @@ DH_DEV fp from_vec(const fpvec& v) {
 }
 
 DH_DEV fp fp_mul(const fp& a, const fp& b) {
+  DH_COUNT_PROD();
 #ifdef DH_MUL_INLINE
   fp r;
   m28::mul(r.v, a.v, b.v);
@@ -268,6 +269,7 @@ DH_DEV fp fp_mul(const fp& a, const fp& b) {
 }
 
 DH_DEV fp fp_sqr(const fp& a) {
+  DH_COUNT_PROD();
 #ifdef DH_MUL_INLINE
   fp r;
   m28::sqr(r.v, a.v);
@@ -333,11 +335,13 @@ struct fp28 {
   uint32_t l[14];
 };
 DH_DEV fp28 fp28_mul(const fp28& a, const fp28& b) {
+  DH_COUNT_PROD();
   fp28 r;
   m28::mont_mul(r.l, a.l, b.l);
   return r;
 }
 DH_DEV fp28 fp28_sqr(const fp28& a) {
+  DH_COUNT_PROD();
   fp28 r;
   m28::mont_sqr(r.l, a.l);
   return r;

@@ -38,11 +38,13 @@ DH_DEV f28 f28_unvec(const fp28vec& v) {
 }
 
 DH_DEV f28 f28_mul(const f28& a, const f28& b) {
+  DH_COUNT_PROD();
   fp28vec x = f28_vec(a), y = f28_vec(b);
   asm(DH_FP_CALL("dh_fp28_mul_vec") : "+{v[0:15]}"(x), "+{v[16:31]}"(y) : : DH_FP28_CALL_CLOBBERS);
   return f28_unvec(x);
 }
 DH_DEV f28 f28_sqr(const f28& a) {
+  DH_COUNT_PROD();
   fp28vec x = f28_vec(a);
   asm(DH_FP_CALL("dh_fp28_sqr_vec")
       : "+{v[0:15]}"(x)
@@ -180,11 +182,13 @@ struct j28 {
 // the products inlined (fp_mul28.hpp), for the doubling that makes up the subgroup test's loops: the compiler
 // allocates its operands freely instead of moving them into the call's fixed registers
 DH_DEV f28 f28_mul_inl(const f28& a, const f28& b) {
+  DH_COUNT_PROD();
   f28 r;
   m28::mont_mul(r.l, a.l, b.l);
   return r;
 }
 DH_DEV f28 f28_sqr_inl(const f28& a) {
+  DH_COUNT_PROD();
   f28 r;
   m28::mont_sqr(r.l, a.l);
   return r;
@@ -275,6 +279,57 @@ DH_DEV j28 j28_add(const j28& p, const j28& q) {
   r.z = f28_mul(zz, h);                                                // 6 x 4 -> < 2
   return r;
 }
+
+// The MSM's bucket additions (k_msm.hip) use the two formulas above WITHOUT their exceptional-case tests (one
+// product each): when h = 0 mod p (the added point equals the accumulator or its negative) Z3 = 2 Z1 H (madd) or
+// 2 Z1 Z2 H (add) vanishes mod p, and every later step keeps Z = 0 mod p (madd: Z3 = 2 Z1 H, add: 2 Z1 Z2 H, dbl:
+// 2 Y Z, whatever the other operand). So ONE zero test of Z at the end of a run of additions (j28_poisoned) finds
+// every run that met such a case, and that run is recomputed with the exact formulas. Same bounds as the exact ones.
+DH_DEV j28 j28_madd_fast(const j28& p, const f28& qx, const f28& qy) {
+  if (p.inf) return j28{qx, qy, f28_one(), false};
+  const f28 z1z1 = f28_sqr(p.z);
+  const f28 u2 = f28_mul(qx, z1z1);
+  const f28 s2 = f28_mul(f28_mul(qy, p.z), z1z1);
+  const f28 h = f28_sub<26>(u2, p.x);
+  const f28 rr = f28_sub<18>(s2, p.y);
+  const f28 hh = f28_sqr(h);
+  const f28 i = f28_scale(hh, 4);
+  const f28 j = f28_mul(h, i);
+  const f28 r2 = f28_scale(rr, 2);
+  const f28 v = f28_mul(p.x, i);
+  j28 r;
+  r.inf = false;
+  r.x = f28_lin3<6>(f28_sqr(r2), 1, j, -1, v, -2);
+  const f28 m = f28_mul(r2, f28_sub<8>(v, r.x));
+  r.y = f28_lin<4>(m, 1, f28_mul(p.y, j), -2);
+  r.z = f28_lin3<4>(f28_sqr(f28_add(p.z, h)), 1, z1z1, -1, hh, -1);
+  return r;
+}
+DH_DEV j28 j28_add_fast(const j28& p, const j28& q) {
+  if (p.inf) return q;
+  if (q.inf) return p;
+  const f28 z1z1 = f28_sqr(p.z), z2z2 = f28_sqr(q.z);
+  const f28 u1 = f28_mul(p.x, z2z2), u2 = f28_mul(q.x, z1z1);
+  const f28 s1 = f28_mul(f28_mul(p.y, q.z), z2z2);
+  const f28 s2 = f28_mul(f28_mul(q.y, p.z), z1z1);
+  const f28 h = f28_sub<2>(u2, u1);
+  const f28 rr = f28_sub<2>(s2, s1);
+  const f28 i = f28_sqr(f28_scale(h, 2));
+  const f28 j = f28_mul(h, i);
+  const f28 r2 = f28_scale(rr, 2);
+  const f28 v = f28_mul(u1, i);
+  j28 r;
+  r.inf = false;
+  r.x = f28_lin3<6>(f28_sqr(r2), 1, j, -1, v, -2);
+  const f28 m = f28_mul(r2, f28_sub<8>(v, r.x));
+  r.y = f28_lin<4>(m, 1, f28_mul(s1, j), -2);
+  const f28 zz = f28_lin3<4>(f28_sqr(f28_add(p.z, q.z)), 1, z1z1, -1, z2z2, -1);
+  r.z = f28_mul(zz, h);
+  return r;
+}
+DH_DEV bool j28_poisoned(const j28& p) { return !p.inf && f28_zero(p.z); }
+// -y for a y < 2p (loaded points): 2p - y
+DH_DEV f28 f28_neg2(const f28& y) { return f28_lin<2>(y, -1, y, 0); }
 
 // G1 subgroup test of an affine point (curve.hpp / codec.hpp g1_in_subgroup, same algorithm): phi(P) == -[u^2] P
 // with [u^2] P = [|u|]([|u|] P), |u| = 0xd201000000010000. ld() returns P; it is called at the start and again

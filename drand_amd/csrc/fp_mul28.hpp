@@ -24,6 +24,25 @@
 #include <stdint.h>
 
 namespace dh {
+
+// Counting build (make -C drand_amd count -> libdrandhip_count.so): every field product or squaring a lane executes
+// bumps a per-translation-unit device counter, read back by the host after each profiled launch
+// (dh_profile_read "products"; bench/count_products.py -> bench/workmodel.json). The regular build compiles nothing.
+#ifdef DH_COUNT_PRODUCTS
+static __device__ unsigned long long dh_nprod;
+#define DH_COUNT_PROD() atomicAdd(&dh_nprod, 1ull)
+#define DH_COUNTER_ACCESSOR(tu)                                                  \
+  hipError_t count_take_##tu(unsigned long long* v) {                            \
+    hipError_t e = hipMemcpyFromSymbol(v, HIP_SYMBOL(dh_nprod), sizeof *v);      \
+    if (e != hipSuccess) return e;                                               \
+    const unsigned long long z = 0;                                              \
+    return hipMemcpyToSymbol(HIP_SYMBOL(dh_nprod), &z, sizeof z);                \
+  }
+#else
+#define DH_COUNT_PROD() ((void)0)
+#define DH_COUNTER_ACCESSOR(tu)
+#endif
+
 namespace m28 {
 constexpr uint32_t MASK = 0x0fffffffu;
 constexpr uint32_t N0 = 0x0ffcfffdu;  // -p^-1 mod 2^28

@@ -132,4 +132,6 @@ hipError_t launch_leaf_check(int sig_g2, const uint32_t* entries, size_t m, cons
 }
 
 
+DH_COUNTER_ACCESSOR(check)
+
 }  // namespace dh

@@ -445,6 +445,304 @@ hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, si
   return hipMemcpyAsync(outB, ws.out2 + ngroups * jw, bytes, hipMemcpyDeviceToDevice, st);
 }
 
+// ================================================================ the RLC MSM in the lazily reduced 28-bit form (G1)
+// Points enter once in the 28-bit form (k_msm_prep28: sigma affine, the hash points Jacobian, each with its
+// endomorphism image at index n + i) and every addition of the bucket pass, the fix-up, the bucket reduction and the
+// window Horner runs on fp28.hpp's lazy values: no 12 <-> 14 limb slicing or final subtraction per product, no
+// modular reduction per sum. The bucket pass uses the formulas without exceptional-case tests and one zero test of Z
+// per run (j28_poisoned); the rare poisoned run is recomputed with the exact formulas. Stored elements take 16 words
+// (14 limbs + 2 pad: four 16-byte loads); a Jacobian point 48 words, infinity stored as Z = 0 (all limbs zero: a
+// finite point's Z is never 0 mod p). The window sums leave in the 12 x 32-bit Montgomery Jacobian form the checks read.
+constexpr int W28 = 16;
+DH_DEV f28 ld28(const uint32_t* p) {
+  const uint4* q = (const uint4*)p;
+  f28 a;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint4 t = q[i];
+    a.l[4 * i] = t.x;
+    a.l[4 * i + 1] = t.y;
+    if (4 * i + 2 < 14) a.l[4 * i + 2] = t.z;
+    if (4 * i + 3 < 14) a.l[4 * i + 3] = t.w;
+  }
+  return a;
+}
+DH_DEV void st28(uint32_t* p, const f28& a) {
+  uint4* q = (uint4*)p;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    q[i] = make_uint4(a.l[4 * i], a.l[4 * i + 1], 4 * i + 2 < 14 ? a.l[4 * i + 2] : 0u, 4 * i + 3 < 14 ? a.l[4 * i + 3] : 0u);
+}
+DH_DEV j28 ldj28(const uint32_t* base, size_t i) {
+  const uint32_t* p = base + (size_t)3 * W28 * i;
+  j28 r;
+  r.x = ld28(p);
+  r.y = ld28(p + W28);
+  r.z = ld28(p + 2 * W28);
+  uint32_t nz = 0;
+#pragma unroll
+  for (int k = 0; k < 14; k++) nz |= r.z.l[k];
+  r.inf = nz == 0;
+  return r;
+}
+DH_DEV void stj28(uint32_t* base, size_t i, const j28& a) {
+  uint32_t* p = base + (size_t)3 * W28 * i;
+  st28(p, a.x);
+  st28(p + W28, a.y);
+  f28 z = a.z;
+  if (a.inf) {
+#pragma unroll
+    for (int k = 0; k < 14; k++) z.l[k] = 0;
+  }
+  st28(p + 2 * W28, z);
+}
+
+// beta (phi(x, y) = (beta x, y) on G1) as a 28-bit Montgomery constant (beta R' mod p)
+__device__ __constant__ uint32_t BETA28[14] = {0xa75929au, 0x681b798u, 0x22a3e9du, 0xabc02bfu, 0x4e5bb45u, 0x55e6e7eu, 0x4814117u,
+                                               0x6d04f1bu, 0xae3387du, 0x54acb0cu, 0x0a4c74bu, 0x56138b5u, 0xb64e066u, 0x00076f2u};
+
+// sigma_i (affine, 12 x 32) -> S[i], S[n + i] = phi(sigma_i); Q_i (Jacobian, 12 x 32) -> Q[i], Q[n + i] = phi(Q_i)
+__global__ __launch_bounds__(256, 2) void k_msm_prep28_g1(size_t n, const uint8_t* __restrict__ status,
+                                                          const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ q_pts,
+                                                          uint32_t* __restrict__ S, uint32_t* __restrict__ Q) {
+  const size_t i = gtid();
+  if (i >= n || status[i] != DEC_OK) return;
+  const f28 beta = f28_c(BETA28);
+  {
+    const aff<fp> a = ld_aff_aos<fp>(sig_aff, i);
+    const f28 x = f28_from_fp(a.x), y = f28_from_fp(a.y);
+    st28(S + 2 * W28 * i, x);
+    st28(S + 2 * W28 * i + W28, y);
+    st28(S + 2 * W28 * (n + i), f28_mul(x, beta));
+    st28(S + 2 * W28 * (n + i) + W28, y);
+  }
+  const jac<fp> q = ld_jac_aos<fp>(q_pts, i);
+  j28 h;
+  h.x = f28_from_fp(q.x);
+  h.y = f28_from_fp(q.y);
+  h.z = f28_from_fp(q.z);
+  h.inf = fp_is_zero(q.z);
+  stj28(Q, i, h);
+  h.x = f28_mul(h.x, beta);
+  stj28(Q, n + i, h);
+}
+
+// sum of the listed entries [a, b] of one key with the exact formulas (a poisoned run, or its recomputation)
+template <bool AFFINE>
+DH_DEV j28 bucket_run_exact28(const uint32_t* __restrict__ list, uint32_t a, uint32_t b, const uint32_t* __restrict__ pts,
+                              const uint8_t* __restrict__ skip, uint32_t nround) {
+  j28 acc = j28_inf();
+#pragma unroll 1
+  for (uint32_t j = a; j <= b; j++) {
+    const uint32_t raw = list[j];
+    const uint32_t idx = raw & ~NEG_BIT;
+    if (skip && skip[idx < nround ? idx : idx - nround] != DEC_OK) continue;
+    if constexpr (AFFINE) {
+      const f28 x = ld28(pts + 2 * W28 * idx);
+      f28 y = ld28(pts + 2 * W28 * idx + W28);
+      if (raw & NEG_BIT) y = f28_neg2(y);
+      acc = j28_madd(acc, x, y);
+    } else {
+      j28 q = ldj28(pts, idx);
+      if (raw & NEG_BIT) q.y = f28_neg2(q.y);
+      acc = j28_add(acc, q);
+    }
+  }
+  return acc;
+}
+
+// the balanced bucket pass of k_msm_bucket (same chunking, partials and metadata) on 28-bit points
+template <bool AFFINE>
+__global__ __launch_bounds__(256, 2) void k_msm_bucket28(const uint32_t* __restrict__ off, const uint32_t* __restrict__ list,
+                                                         size_t nkeys, uint32_t L, const uint32_t* __restrict__ pts,
+                                                         uint32_t* __restrict__ buckets, uint32_t* __restrict__ part,
+                                                         uint32_t* __restrict__ meta, const uint8_t* __restrict__ skip,
+                                                         uint32_t nround) {
+  const size_t t = gtid();
+  const uint32_t total = off[nkeys];
+  const size_t s = t * (size_t)L;
+  if (s >= total) return;
+  const uint32_t e = (uint32_t)min(s + L, (size_t)total);
+  size_t lo = 0, hi = nkeys;
+  while (hi - lo > 1) {
+    size_t mid = (lo + hi) >> 1;
+    if (off[mid] <= s) lo = mid;
+    else hi = mid;
+  }
+  size_t key = lo;
+  uint32_t kend = off[key + 1];
+  const bool starts_before = off[key] < s;
+  bool first = true;
+  uint32_t head_kind = 0, tail_key = NO_KEY, run0 = (uint32_t)s;
+  j28 acc = j28_inf();
+#pragma unroll 1
+  for (uint32_t j = (uint32_t)s; j < e; j++) {
+    const uint32_t raw = list[j];
+    const uint32_t idx = raw & ~NEG_BIT;
+    if (!skip || skip[idx < nround ? idx : idx - nround] == DEC_OK) {
+      if constexpr (AFFINE) {
+        const f28 x = ld28(pts + 2 * W28 * idx);
+        f28 y = ld28(pts + 2 * W28 * idx + W28);
+        if (raw & NEG_BIT) y = f28_neg2(y);
+        acc = j28_madd_fast(acc, x, y);
+      } else {
+        j28 q = ldj28(pts, idx);
+        if (raw & NEG_BIT) q.y = f28_neg2(q.y);
+        acc = j28_add_fast(acc, q);
+      }
+    }
+    const bool ends = j + 1 == kend;
+    if (ends || j + 1 == e) {
+      if (j28_poisoned(acc)) acc = bucket_run_exact28<AFFINE>(list, run0, j, pts, skip, nround);
+      if (first && starts_before) {
+        stj28(part, 2 * t, acc);
+        head_kind = ends ? 1 : 2;
+      } else if (ends) {
+        stj28(buckets, key, acc);
+      } else {
+        stj28(part, 2 * t + 1, acc);
+        tail_key = (uint32_t)key;
+      }
+      first = false;
+      run0 = j + 1;
+      if (ends && j + 1 < e) {
+        do {
+          key++;
+        } while (off[key + 1] <= j + 1);
+        kend = off[key + 1];
+        acc = j28_inf();
+      }
+    }
+  }
+  if (meta) {
+    meta[2 * t] = head_kind;
+    meta[2 * t + 1] = tail_key;
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void k_msm_bucket_fix28(const uint32_t* __restrict__ off, size_t nkeys, uint32_t L,
+                                                             const uint32_t* __restrict__ meta, const uint32_t* __restrict__ part,
+                                                             uint32_t* __restrict__ buckets) {
+  const size_t t = gtid();
+  const uint32_t total = off[nkeys];
+  const size_t nch = (total + L - 1) / L;
+  if (t >= nch) return;
+  const uint32_t key = meta[2 * t + 1];
+  if (key == NO_KEY) return;
+  j28 acc = ldj28(part, 2 * t + 1);
+#pragma unroll 1
+  for (size_t u = t + 1; u < nch; u++) {
+    acc = j28_add(acc, ldj28(part, 2 * u));
+    if (meta[2 * u] == 1) break;
+  }
+  stj28(buckets, key, acc);
+}
+
+// per (set, group, window, segment): sum_{d in seg} d B_d; a bucket whose key holds no entry is the identity and is not
+// read (the bucket array is never cleared). Rows of both point sets share the keys: row gw -> key row gw % rows_per_set.
+__global__ __launch_bounds__(256, 2) void k_msm_segsum28(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ off,
+                                                         msm_geom g, size_t ngw, size_t rows_per_set, uint32_t* __restrict__ segs) {
+  const size_t t = gtid();
+  if (t >= ngw * g.nseg) return;
+  const size_t gw = t / g.nseg;
+  const uint32_t s = t % g.nseg;
+  const uint32_t a = 1 + s * g.seglen;
+  uint32_t last = a + g.seglen;
+  if (last > g.nbuck) last = g.nbuck;
+  const size_t krow = (gw % rows_per_set) * g.nbuck;
+  j28 run = j28_inf(), tot = j28_inf();
+#pragma unroll 1
+  for (int d = (int)last - 1; d >= (int)a; d--) {
+    if (off[krow + d + 1] != off[krow + d]) run = j28_add(run, ldj28(buckets, gw * g.nbuck + d));
+    tot = j28_add(tot, run);
+  }
+  const uint32_t k = a - 1;
+  if (k && !run.inf) {
+    j28 acc = j28_inf();
+#pragma unroll 1
+    for (int bit = 31 - __builtin_clz(k); bit >= 0; bit--) {
+      acc = j28_dbl(acc);
+      if ((k >> bit) & 1) acc = j28_add(acc, run);
+    }
+    tot = j28_add(tot, acc);
+  }
+  stj28(segs, t, tot);
+}
+
+__global__ __launch_bounds__(256, 2) void k_msm_tree28(uint32_t* __restrict__ v, size_t rows, uint32_t stride, uint32_t width,
+                                                       uint32_t half) {
+  const size_t t = gtid();
+  if (t >= rows * half) return;
+  const size_t r = t / half, c = t % half;
+  if (c + half >= width) return;
+  const size_t i = r * stride + c;
+  stj28(v, i, j28_add(ldj28(v, i), ldj28(v, i + half)));
+}
+
+// per (set, group): Horner over the windows, out = 12 x 32-bit Montgomery Jacobian (jac_inf for the identity)
+__global__ __launch_bounds__(64) void k_msm_windows28(const uint32_t* __restrict__ segs, msm_geom g, size_t ngroups,
+                                                      uint32_t* __restrict__ out) {
+  const size_t t = gtid();
+  if (t >= ngroups) return;
+  j28 acc = ldj28(segs, (t * g.nwin + g.nwin - 1) * g.nseg);
+#pragma unroll 1
+  for (int w = g.nwin - 2; w >= 0; w--) {
+#pragma unroll 1
+    for (int k = 0; k < g.c; k++) acc = j28_dbl(acc);
+    acc = j28_add(acc, ldj28(segs, (t * g.nwin + w) * g.nseg));
+  }
+  jac<fp> r = jac_inf<fp>();
+  if (!acc.inf) {
+    r.x = f28_to_fp(acc.x);
+    r.y = f28_to_fp(acc.y);
+    r.z = f28_to_fp(acc.z);
+  }
+  st_jac_aos<fp>(out, t, r);
+}
+
+hipError_t launch_msm_prep28(int sig_g2, size_t n, const uint8_t* status, const uint32_t* sig_aff, const uint32_t* q_pts,
+                             uint32_t* S, uint32_t* Q, hipStream_t st) {
+  if (sig_g2) return hipErrorInvalidValue;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_msm_prep28_g1, dim3(nblk(n, 256)), dim3(256), 0, st, n, status, sig_aff, q_pts, S, Q);
+  return hipGetLastError();
+}
+
+// launch_msm on the 28-bit points of launch_msm_prep28 (G1): both point sets, one reduction pass over 2 x ngroups
+hipError_t launch_msm28(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
+                        const uint32_t* S, const uint32_t* Q, msm_ws& ws, uint32_t* outA, uint32_t* outB, hipStream_t st,
+                        const uint8_t* skip, bool presorted) {
+  if (sig_g2) return hipErrorInvalidValue;
+  hipError_t e = hipSuccess;
+  if (!presorted && (e = launch_msm_sort(g, entries, nullptr, nullptr, m, ngroups, scal, ws, st)) != hipSuccess) return e;
+  const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
+  constexpr size_t jw = 3 * W28;
+  uint32_t* bB = ws.buckets + nk * jw;
+  uint32_t* pB = ws.part + msm_nchunks(ws.max_entries) * 2 * jw;
+  if (ws.max_entries) {
+    const uint32_t L = msm_chunk_len(ws.max_entries);
+    const size_t nch = (ws.max_entries + L - 1) / L;
+    hipLaunchKernelGGL((k_msm_bucket28<true>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, S, ws.buckets,
+                       ws.part, ws.meta, skip, g.half_stride);
+    hipLaunchKernelGGL(k_msm_bucket_fix28, dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, nk, L, ws.meta, ws.part, ws.buckets);
+    hipLaunchKernelGGL((k_msm_bucket28<false>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, Q, bB, pB,
+                       ws.meta, skip, g.half_stride);
+    hipLaunchKernelGGL(k_msm_bucket_fix28, dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, nk, L, ws.meta, pB, bB);
+  }
+  const size_t rows = ngroups * g.nwin, ngw = 2 * rows;
+  hipLaunchKernelGGL(k_msm_segsum28, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs);
+  for (uint32_t width = g.nseg; width > 1;) {
+    const uint32_t half = (width + 1) / 2;
+    hipLaunchKernelGGL(k_msm_tree28, dim3(nblk(ngw * half, 256)), dim3(256), 0, st, ws.segs, ngw, g.nseg, width, half);
+    width = half;
+  }
+  hipLaunchKernelGGL(k_msm_windows28, dim3(nblk(2 * ngroups, 64)), dim3(64), 0, st, ws.segs, g, 2 * ngroups, ws.out2);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const size_t bytes = ngroups * 36 * 4;
+  if ((e = hipMemcpyAsync(outA, ws.out2, bytes, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
+  return hipMemcpyAsync(outB, ws.out2 + ngroups * 36, bytes, hipMemcpyDeviceToDevice, st);
+}
+
 hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,
                               uint8_t* verdict, hipStream_t st) {
   if (!m) return hipSuccess;
@@ -452,5 +750,7 @@ hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, c
   return hipGetLastError();
 }
 
+
+DH_COUNTER_ACCESSOR(msm)
 
 }  // namespace dh

@@ -276,4 +276,6 @@ hipError_t launch_hash(int sig_g2, const uint64_t* rounds, const uint8_t* prevs,
   return hipGetLastError();
 }
 
+DH_COUNTER_ACCESSOR(prep)
+
 }  // namespace dh

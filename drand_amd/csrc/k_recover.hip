@@ -419,4 +419,6 @@ hipError_t launch_recover_pairs(int sig_g2, const uint32_t* shares, const uint32
   return hipGetLastError();
 }
 
+DH_COUNTER_ACCESSOR(recover)
+
 }  // namespace dh

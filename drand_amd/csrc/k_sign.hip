@@ -121,4 +121,6 @@ hipError_t launch_pubkey(int key_g2, const uint32_t* sk, uint8_t* out, hipStream
   return hipGetLastError();
 }
 
+DH_COUNTER_ACCESSOR(sign)
+
 }  // namespace dh

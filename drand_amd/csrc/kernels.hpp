@@ -71,6 +71,14 @@ hipError_t launch_scan(const uint32_t* cnt, size_t nk, uint32_t* off, uint32_t* 
 hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
                       const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
                       hipStream_t st, const uint8_t* skip = nullptr, bool presorted = false);
+// the same MSM on the lazily reduced 28-bit points (k_msm.hip MSM28; G1): launch_msm_prep28 converts the batch's
+// sigma (affine) and hash points (Jacobian) with their endomorphism images into S (32 words per point) and Q (48 words
+// per point), 2n points each; the workspace's bucket / partial / segment arrays hold 48-word points
+hipError_t launch_msm_prep28(int sig_g2, size_t n, const uint8_t* status, const uint32_t* sig_aff, const uint32_t* q_pts,
+                             uint32_t* S, uint32_t* Q, hipStream_t st);
+hipError_t launch_msm28(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
+                        const uint32_t* S, const uint32_t* Q, msm_ws& ws, uint32_t* outA, uint32_t* outB, hipStream_t st,
+                        const uint8_t* skip, bool presorted);
 hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp, size_t m,
                            size_t ngroups, const uint4* scal, msm_ws& ws, hipStream_t st);
 hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngroups, const uint32_t* pts, msm_ws& ws,
@@ -126,5 +134,15 @@ hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam,
 hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, hipStream_t st);
 hipError_t launch_recover_pairs(int sig_g2, const uint32_t* shares, const uint32_t* B, const uint32_t* A, int n_nodes,
                                 uint32_t* P, uint32_t* Q, hipStream_t st);
+
+#ifdef DH_COUNT_PRODUCTS
+// counting build: field products executed since the last take, per translation unit (fp_mul28.hpp)
+hipError_t count_take_prep(unsigned long long* v);
+hipError_t count_take_msm(unsigned long long* v);
+hipError_t count_take_check(unsigned long long* v);
+hipError_t count_take_sign(unsigned long long* v);
+hipError_t count_take_recover(unsigned long long* v);
+hipError_t count_take_vm(unsigned long long* v);
+#endif
 
 }  // namespace dh

@@ -105,3 +105,54 @@ def iso11(X32,Y32,Z32,xnum,xden,ynum,yden):
         if j<len(xden): xd=add(mont(xd,X),mont(c(xden[-1-j]),zp))
     a=mont(xd,D); z3=mont(D,Zp); ydz3=mont(yd,z3); rz=mont(a,ydz3)
     return (to_fp(mont(mont(xn,ydz3),rz)), to_fp(mont(mont(mont(f(Y32),yn),a),mont(rz,rz))), to_fp(rz))
+
+# ---- the MSM's bucket additions (k_msm.hip MSM28): the same formulas without the exceptional-case tests, and the
+# run-level zero test of Z that sends a poisoned run back through the exact formulas (fp28.hpp j28_madd_fast etc.)
+def madd_fast(P,qx,qy):
+    X,Y,Z,fl=P
+    if fl: return (qx,qy,ONE,False)
+    z1z1=mont(Z,Z); u2=mont(qx,z1z1); s2=mont(mont(qy,Z),z1z1)
+    h=sub(26,u2,X); rr=sub(18,s2,Y)
+    hh=mont(h,h); i=scale(hh,4); j=mont(h,i); r2=scale(rr,2); v=mont(X,i)
+    x=lin3(6,mont(r2,r2),1,j,-1,v,-2)
+    m=mont(r2,sub(8,v,x)); y=lin(4,m,1,mont(Y,j),-2)
+    zs=add(Z,h); z=lin3(4,mont(zs,zs),1,z1z1,-1,hh,-1)
+    return (x,y,z,False)
+def jadd_fast(P,Q):
+    X1,Y1,Z1,f1=P; X2,Y2,Z2,f2=Q
+    if f1: return Q
+    if f2: return P
+    z1z1=mont(Z1,Z1); z2z2=mont(Z2,Z2); u1=mont(X1,z2z2); u2=mont(X2,z1z1)
+    s1=mont(mont(Y1,Z2),z2z2); s2=mont(mont(Y2,Z1),z1z1)
+    h=sub(2,u2,u1); rr=sub(2,s2,s1)
+    h2=scale(h,2); i=mont(h2,h2); j=mont(h,i); r2=scale(rr,2); v=mont(u1,i)
+    x=lin3(6,mont(r2,r2),1,j,-1,v,-2)
+    m=mont(r2,sub(8,v,x)); y=lin(4,m,1,mont(s1,j),-2)
+    zs=add(Z1,Z2); zz=lin3(4,mont(zs,zs),1,z1z1,-1,z2z2,-1); z=mont(zz,h)
+    return (x,y,z,False)
+def poisoned(P): return (not P[3]) and zero(P[2])
+def neg2(y): return lin(2,y,-1,y,0)
+def bucket_run(pts, affine):
+    """k_msm_bucket28 on one run: pts = [(x28, y28) or (X, Y, Z) 28-bit, neg flag]; returns (sum, was_poisoned)."""
+    acc=inf()
+    for pt,neg in pts:
+        if affine:
+            x,y=pt; acc=madd_fast(acc,x,neg2(y) if neg else y)
+        else:
+            X,Y,Z=pt; acc=jadd_fast(acc,(X,neg2(Y) if neg else Y,Z,Z==0))
+    if not poisoned(acc):
+        return acc,False
+    acc=inf()
+    for pt,neg in pts:
+        if affine:
+            x,y=pt; acc=madd(acc,x,neg2(y) if neg else y)
+        else:
+            X,Y,Z=pt; acc=jadd(acc,(X,neg2(Y) if neg else Y,Z,Z==0))
+    return acc,True
+def to_affine(P):
+    """normal-field affine point of a model Jacobian point (None = infinity)"""
+    X,Y,Z,fl=P
+    if fl: return None
+    f=lambda v: v*pow(RP,-1,p)%p
+    z=f(Z); zi=pow(z,-1,p)
+    return (f(X)*zi*zi%p, f(Y)*zi**3%p)

@@ -53,3 +53,45 @@ def test_fp28_isogeny_model_matches_oracle():
             continue
         zi = pow(norm(Zo), -1, p)
         assert (norm(Xo) * zi * zi % p, norm(Yo) * zi ** 3 % p) == want
+
+
+def test_msm28_bucket_runs_match_oracle():
+    """k_msm_bucket28's runs (fast formulas + one zero test of Z per run, exact recomputation when poisoned) on the
+    model: random runs of G1 points and their negatives (affine and Jacobian inputs) give the oracle's sums, and the
+    exceptional runs — a point added to itself, a point and its negative, a run summing to the identity — are the
+    ones flagged poisoned. Every product / sum bound is asserted along the way."""
+    rng = random.Random(13)
+    g = B.G1_GEN
+    pts = [B.ec_mul(B.FP, g, rng.randrange(1, R)) for _ in range(6)]
+    enc = lambda P: (M.from_fp(P[0]), M.from_fp(P[1]))  # noqa: E731
+
+    def jac(P):  # a random Jacobian representative (Z != 1), as the hash points arrive
+        z = rng.randrange(2, M.p)
+        X, Y, Z = P[0] * z * z % M.p, P[1] * z ** 3 % M.p, z
+        return (M.from_fp(X), M.from_fp(Y), M.from_fp(Z))
+
+    def oracle_sum(run):
+        acc = None
+        for P, neg in run:
+            acc = B.ec_add(B.FP, acc, (P[0], (-P[1]) % M.p) if neg else P)
+        return acc
+
+    runs = [[(pts[k % 6], rng.random() < 0.5) for k in rng.sample(range(60), 9)] for _ in range(4)]
+    exceptional = [[(pts[0], False), (pts[0], False)], [(pts[1], False), (pts[1], True), (pts[2], False)],
+                   [(pts[3], False), (pts[3], True)],
+                   [(pts[4], False), (pts[5], False), (B.ec_add(B.FP, pts[4], pts[5]), True)]]
+    for run in runs + exceptional:
+        for affine in (True, False):
+            got, pois = M.bucket_run([(enc(P) if affine else jac(P), neg) for P, neg in run], affine)
+            assert M.to_affine(got) == oracle_sum(run)
+            if run in exceptional:
+                assert pois
+    # the poison persists: once Z = 0 mod p, more fast additions keep it
+    acc = M.madd_fast(M.madd_fast(M.inf(), *enc(pts[0])), *enc(pts[0]))
+    for P in pts[1:]:
+        assert M.poisoned(acc)
+        acc = M.madd_fast(acc, *enc(P))
+        acc = M.jadd_fast(acc, (*jac(P), False))
+        acc = M.jadd_fast((*jac(P), False), acc)
+        acc = M.dbl(acc)
+    assert M.poisoned(acc)
