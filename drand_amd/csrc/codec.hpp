@@ -13,6 +13,7 @@
 #pragma once
 #include "h2c.hpp"
 #include "fp28.hpp"
+#include "fp2_28.hpp"
 
 namespace dh {
 
@@ -41,9 +42,8 @@ DH_DEV bool g1_in_subgroup(const aff<fp>& p) {
 }
 
 DH_DEV bool g2_in_subgroup(const aff<fp2>& p) {
-  // [u] P = -[|u|] P
-  jac<fp2> t = jac_neg(jac_mul_uabs(p));
-  return jac_eq(g2_psi(jac_from_aff(p)), t);
+  // psi(P) == [u] P = -[|u|] P, on lazily reduced 28-bit limbs (fp2_28.hpp)
+  return g2_in_subgroup28(p);
 }
 
 // decode a 48-byte compressed G1 point (4-byte aligned); optional subgroup check

@@ -94,6 +94,8 @@ struct worker {
   dbuf status, sig_aff, q_pts, scal, entries, verdict_tmp, rand_tmp, h2c_tmp;
   // the MSM's 28-bit points (launch_msm_prep28, G1): sigma and its phi image (32 words each), hash points (48 words)
   dbuf s28, q28;
+  // bisection on the device: the next level's entries, fail flags, their ranks and the scan's block sums
+  dbuf entries_alt, cflags, crank, cscan;
   // host-API staging
   dbuf in_rounds, in_sigs, in_prevs, in_prev_lens, out_verdict, out_rand;
   // key
@@ -106,16 +108,14 @@ struct worker {
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
       r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den;
-  std::vector<uint8_t> h_pass;
   std::vector<uint8_t> h_verdict;
   // decoded group key cache: the same key is used for every batch of a chain
   uint8_t cached_key[96];
   size_t cached_key_len = 0;
   int cached_key_g2 = -1;
   uint8_t cached_key_ok = 0;
-  std::vector<uint32_t> h_entries, h_next;
   void release_all() {
-    dbuf* all[] = {&s28, &q28, &status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &h2c_tmp, &in_rounds, &in_sigs,
+    dbuf* all[] = {&s28, &q28, &entries_alt, &cflags, &crank, &cscan, &status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &h2c_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
@@ -422,6 +422,14 @@ static bool lane_pairing() {
   return v;
 }
 
+static bool msm32_selected() {
+  static const bool v = [] {
+    const char* e = getenv("DRANDHIP_MSM32");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // key_h: [h_eff] pk next to a decoded G2 key (k_decode_key), or null (the check clears B's cofactor itself)
 static hipError_t group_check(worker* w, bool g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key,
                               uint8_t* pass, hipStream_t st, const uint32_t* key_h = nullptr) {
@@ -534,7 +542,8 @@ static int msm_workspace(worker* w, const dh::msm_geom& g, size_t m, size_t ngro
   HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
   HIP_TRY(w->list.ensure(dh::msm_entries(g, m) * 4));
   HIP_TRY(w->buckets.ensure(2 * nk * jw * 4));
-  HIP_TRY(w->segs.ensure(2 * ngroups * g.nwin * g.nseg * jw * 4));
+  const size_t segs_bytes = 2 * ngroups * g.nwin * g.nseg * jw * 4;
+  HIP_TRY(w->segs.ensure(2 * segs_bytes));  // segment sums, then (MSM28) the segments' running sums
   HIP_TRY(w->outA.ensure(ngroups * jw * 4));
   HIP_TRY(w->outB.ensure(ngroups * jw * 4));
   HIP_TRY(w->out2.ensure(2 * ngroups * jw * 4));
@@ -543,7 +552,7 @@ static int msm_workspace(worker* w, const dh::msm_geom& g, size_t m, size_t ngro
   HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(dh::msm_entries(g, m))));
   ws = dh::msm_ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
                   w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>(), w->part.as<uint32_t>(),
-                  w->meta.as<uint32_t>(), 0};
+                  w->meta.as<uint32_t>(), 0, (uint32_t*)((uint8_t*)w->segs.p + segs_bytes)};
   return DH_OK;
 }
 
@@ -561,9 +570,10 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (n >= 0x40000000u) return fail(DH_EINVAL, "batch too large");
   const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
   const size_t aw = jw * 2 / 3;
-  // G1: the MSM runs on lazily reduced 28-bit points (k_msm.hip MSM28), whose workspace points take 48 words
-  const bool msm28 = !g2;
-  const size_t wsw = msm28 ? 48 : jw;
+  // the MSM runs on lazily reduced 28-bit points (k_msm.hip MSM28), whose workspace points take 48 (G1) / 96 (G2)
+  // words; DRANDHIP_MSM32=1 selects the 12 x 32-bit MSM kept as the second implementation
+  const bool msm28 = !msm32_selected();
+  const size_t wsw = msm28 ? (g2 ? 96 : 48) : jw;
 
   timed_launches T(st);
   bool presorted = false;  // level-0 sorted lists already built on the tail stream
@@ -629,10 +639,12 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
       HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), 1, st));
     }
     if (msm28) {
-      HIP_TRY(w->s28.ensure(2 * n * 32 * 4));
-      HIP_TRY(w->q28.ensure(2 * n * 48 * 4));
-      HIP_TRY(dh::launch_msm_prep28(g2, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
-                                    w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), st));
+      HIP_TRY(w->s28.ensure(2 * n * (g2 ? 64 : 32) * 4));
+      HIP_TRY(w->q28.ensure(2 * n * (g2 ? 64 : 32) * 4));
+      HIP_TRY(T.run(g2 ? "k_msm_prep28<fp2>" : "k_msm_prep28<fp>", [&] {
+        return dh::launch_msm_prep28(g2, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
+                                     w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), st);
+      }));
     } else {
       HIP_TRY(dh::launch_endo(g2, n, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(), st));
     }
@@ -721,28 +733,30 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     }
     HIP_TRY(dh::launch_mark_groups(w->entries.as<uint32_t>(), m, gsize, w->pass.as<uint8_t>(), w->status.as<uint8_t>(),
                                    d_verdict, st));
-    w->h_pass.resize(ngroups);
-    HIP_TRY(hipMemcpyAsync(w->h_pass.data(), w->pass.p, ngroups, hipMemcpyDeviceToHost, st));
+    // failing groups' entries compacted on the device; only the failing-group count and the last group's flag
+    // come back to the host (they size the next level)
+    HIP_TRY(w->cflags.ensure(ngroups * 4));
+    HIP_TRY(w->crank.ensure((ngroups + 1) * 4));
+    HIP_TRY(w->cscan.ensure(((ngroups + 4095) / 4096 + 1) * 4));
+    HIP_TRY(w->entries_alt.ensure(m * 4));
+    HIP_TRY(dh::launch_compact_failing(w->entries.as<uint32_t>(), m, gsize, ngroups, w->pass.as<uint8_t>(),
+                                       w->cflags.as<uint32_t>(), w->crank.as<uint32_t>(), w->cscan.as<uint32_t>(),
+                                       w->entries_alt.as<uint32_t>(), st));
+    uint32_t nfail32 = 0;
+    uint8_t last_pass = 1;
+    HIP_TRY(hipMemcpyAsync(&nfail32, w->crank.as<uint32_t>() + ngroups, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&last_pass, w->pass.as<uint8_t>() + ngroups - 1, 1, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     level++;
-    size_t nfail = 0;
-    for (uint8_t p : w->h_pass) nfail += p ? 0 : 1;
+    const size_t nfail = nfail32;
     if (stats) stats[1] += nfail;
     if (nfail == 0) {
       m = 0;
       break;
     }
-    // entries of failing groups, in order
-    w->h_entries.resize(m);
-    HIP_TRY(hipMemcpyAsync(w->h_entries.data(), w->entries.p, m * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    w->h_next.clear();
-    for (size_t gi = 0; gi < ngroups; gi++)
-      if (!w->h_pass[gi])
-        for (size_t e = gi * gsize; e < std::min(m, (gi + 1) * gsize); e++) w->h_next.push_back(w->h_entries[e]);
+    std::swap(w->entries, w->entries_alt);
     const size_t m_prev = m;
-    m = w->h_next.size();
-    HIP_TRY(hipMemcpyAsync(w->entries.p, w->h_next.data(), m * 4, hipMemcpyHostToDevice, st));
+    m = nfail * gsize - (last_pass ? 0 : ngroups * gsize - m_prev);  // only the last group may be short
     gsize = fixed.empty() ? next_group_size(gsize, ngroups, nfail, m_prev, m)
                           : (size_t)(level - 1 < (int)fixed.size() ? fixed[level - 1] : 1);
   }

@@ -79,6 +79,20 @@ DH_KP(24, 0xff80008u, 0xe7fffffu, 0xffff96fu, 0xffe09fdu, 0x362e01fu, 0x1720971u
       0x1834316u, 0x7b9164fu, 0x9e770a9u, 0xdf563fdu, 0x027019au)
 DH_KP(26, 0xff7555eu, 0xe5fffffu, 0x7fff8e3u, 0xffde028u, 0xfab1d77u, 0x590df8fu, 0x07af564u, 0xbb83e77u, 0x41dab80u,
       0xaf8de03u, 0xf0882d5u, 0x6baba0cu, 0x1c9d6fdu, 0x02a41bdu)
+DH_KP(3, 0xfff0001u, 0xfcfffffu, 0xbffff2du, 0xfffc13fu, 0x26c5c03u, 0xe2e412eu, 0xe359277u, 0xda8f383u, 0xd65e28eu,
+      0xe306862u, 0x2f722c9u, 0xb3cee15u, 0x5beac7fu, 0x004e033u)
+DH_KP(7, 0xffdaaadu, 0xf8fffffu, 0xbfffe15u, 0xfff6d94u, 0xafcd6b3u, 0x66bed6bu, 0xbd255c2u, 0xa8a3833u, 0xf4310a2u,
+      0x11b9e3bu, 0x195fbd7u, 0x4e380dcu, 0xd67927fu, 0x00b6077u)
+DH_KP(9, 0xffd0003u, 0xf6fffffu, 0x3fffd89u, 0xfff43bfu, 0x745140bu, 0xa8ac38au, 0xaa0b767u, 0x8fada8bu, 0x831a7acu,
+      0xa913928u, 0x8e5685du, 0x1b6ca3fu, 0x13c057fu, 0x00ea09au)
+DH_KP(12, 0xffc0004u, 0xf3fffffu, 0xffffcb7u, 0xfff04feu, 0x9b1700fu, 0x8b904b8u, 0x8d649dfu, 0x6a3ce0fu, 0x5978a3bu,
+      0x8c1a18bu, 0xbdc8b27u, 0xcf3b854u, 0x6fab1feu, 0x01380cdu)
+DH_KP(21, 0xff90007u, 0xeafffffu, 0x3fffa41u, 0xffe48beu, 0x0f6841bu, 0x343c843u, 0x3770147u, 0xf9ea89bu, 0xdc931e7u,
+      0x352dab3u, 0x4c1f385u, 0xeaa8294u, 0x836b77du, 0x0222167u)
+DH_KP(32, 0xff55560u, 0xdffffffu, 0xffff73fu, 0xffd62a7u, 0x483d57fu, 0x1ed61ecu, 0xce61a54u, 0x70a257eu, 0xee9709eu,
+      0x759aec8u, 0x4f6c869u, 0xd349637u, 0xd472ffcu, 0x0340223u)
+DH_KP(48, 0xff00010u, 0xcffffffu, 0xffff2dfu, 0xffc13fbu, 0x6c5c03fu, 0x2e412e2u, 0x359277eu, 0xa8f383eu, 0x65e28edu,
+      0x306862du, 0xf722c9eu, 0x3cee152u, 0xbeac7fbu, 0x04e0335u)
 #undef DH_KP
 
 // ca a + cb b + K p limb-wise with one signed carry pass. The negative coefficients add up to >= -8 and the positive

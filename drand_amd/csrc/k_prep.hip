@@ -74,8 +74,8 @@ __global__ __launch_bounds__(256, occ<fp2>::W) void k_sub_sig_g2(size_t n, uint8
                                                              uint32_t* __restrict__ sig_aff) {
   size_t i = gtid();
   if (i >= n || status[i] != DEC_OK) return;
-  const aff<fp2> a = ld_aff_aos<fp2>(sig_aff, i);
-  if (!g2_in_subgroup(a)) {
+  // P stays in HBM: the lazy-form test reloads it where it needs its coordinates (fp2_28.hpp g2_in_subgroup28)
+  if (!g2_in_subgroup28([&] { return ld_aff_aos<fp2>(sig_aff, i); })) {
     status[i] = DEC_BAD;
     st_aff_aos<fp2>(sig_aff, i, aff<fp2>{fp2{}, fp2{}});
   }

@@ -36,6 +36,7 @@ struct msm_ws {
   uint32_t* part;      // balanced bucket pass: 2 Jacobian partial sums per chunk (x2 for launch_msm)
   uint32_t* meta;      // balanced bucket pass: 2 words per chunk (head kind, tail key)
   size_t max_entries;  // set by launch_msm_sort: upper bound of sorted-list entries (msm_entries)
+  uint32_t* runs = nullptr;  // MSM28: the segments' running sums (as many points as segs)
 };
 
 // balanced bucket accumulation: entries per chunk, and workspace sizes for `max_entries` list entries
@@ -71,10 +72,11 @@ hipError_t launch_scan(const uint32_t* cnt, size_t nk, uint32_t* off, uint32_t* 
 hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
                       const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
                       hipStream_t st, const uint8_t* skip = nullptr, bool presorted = false);
-// the same MSM on the lazily reduced 28-bit points (k_msm.hip MSM28; G1): launch_msm_prep28 converts the batch's
-// sigma (affine) and hash points (Jacobian) with their endomorphism images into S (32 words per point) and Q (48 words
-// per point), 2n points each; the workspace's bucket / partial / segment arrays hold 48-word points
-hipError_t launch_msm_prep28(int sig_g2, size_t n, const uint8_t* status, const uint32_t* sig_aff, const uint32_t* q_pts,
+// the same MSM on the lazily reduced 28-bit points (k_msm.hip MSM28): launch_msm_prep28 converts the batch's sigma
+// (affine) and hash points (Jacobian, made affine) with their endomorphism images into S and Q (G1 32 / G2 64 words
+// per point, 2n points each; a hash point at infinity marks its round DEC_BAD); the workspace's bucket / partial /
+// segment arrays hold 48 / 96-word Jacobian points
+hipError_t launch_msm_prep28(int sig_g2, size_t n, uint8_t* status, const uint32_t* sig_aff, const uint32_t* q_pts,
                              uint32_t* S, uint32_t* Q, hipStream_t st);
 hipError_t launch_msm28(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
                         const uint32_t* S, const uint32_t* Q, msm_ws& ws, uint32_t* outA, uint32_t* outB, hipStream_t st,
@@ -89,6 +91,10 @@ hipError_t launch_group_check(int sig_g2, const uint32_t* A, const uint32_t* B, 
 hipError_t launch_sum_partials(int sig_g2, const uint32_t* parts, size_t k, uint32_t* outA, uint32_t* outB, hipStream_t st);
 hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,
                               uint8_t* verdict, hipStream_t st);
+// bisection: out = the entries of the groups with pass == 0, in order; rank[ngroups] = the number of failing groups
+// (flags: ngroups words, rank: ngroups + 1, scan_tmp: launch_scan's)
+hipError_t launch_compact_failing(const uint32_t* entries, size_t m, size_t gsize, size_t ngroups, const uint8_t* pass,
+                                  uint32_t* flags, uint32_t* rank, uint32_t* scan_tmp, uint32_t* out, hipStream_t st);
 hipError_t launch_leaf_check(int sig_g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
                              const uint32_t* key_aff, const uint8_t* status, uint8_t* verdict, hipStream_t st);
 

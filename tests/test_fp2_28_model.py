@@ -1,0 +1,126 @@
+"""CPU: the integer model of the lazily reduced 28-bit Fp2 / G2 arithmetic (tests/fp2_28_model.py, mirroring
+drand_amd/csrc/fp2_28.hpp) against the oracle's affine G2 arithmetic (oracle/bls_py.py): Karatsuba products and
+complex squarings, the partial reduction f28_red at its extremes, doubling / mixed / Jacobian additions over long
+chains, the MSM bucket runs with their exceptional cases (fast formulas poison Z, exact recomputation), and the psi
+subgroup test on subgroup points, random curve points and subgroup + torsion sums. Every product input and sum is
+bound-checked by the model, so a formula whose bounds do not hold fails here."""
+import random
+
+import bls_py as B
+import fp28_model as M1
+import fp2_28_model as M
+
+P = M.p
+H2 = 0x5d543a95414e7f1091d50792876a202cd91de4547085abaa68a205b2e5a7ddfa628f1cb4d9e82ef21537e293a6691ae1616ec6e786f0c70cf1c38e31c7238e5
+
+
+def rng_f2(rng):
+    return (rng.randrange(P), rng.randrange(P))
+
+
+def g2_point(rng, subgroup=True):
+    if subgroup:
+        return B.ec_mul(B.FP2, B.G2_GEN, rng.randrange(1, M1.r))
+    while True:
+        x = rng_f2(rng)
+        y = B.f2sqrt(B.f2add(B.f2mul(B.f2mul(x, x), x), B.B2))
+        if y is not None:
+            return (x, y)
+
+
+def enc(pt):
+    return (M.from_f2(pt[0]), M.from_f2(pt[1]))
+
+
+def jac(pt, rng):
+    z = rng_f2(rng)
+    z2 = B.f2mul(z, z)
+    return (M.from_f2(B.f2mul(pt[0], z2)), M.from_f2(B.f2mul(pt[1], B.f2mul(z2, z))), M.from_f2(z), False)
+
+
+def test_fp2_products_and_reduction():
+    rng = random.Random(3)
+    for _ in range(200):
+        a, b = rng_f2(rng), rng_f2(rng)
+        # inputs anywhere inside the bounds the formulas feed them (multiples of p added)
+        A = (M.from_f2(a)[0] + rng.randrange(0, 2) * P, M.from_f2(a)[1] + rng.randrange(0, 4) * P)
+        Bb = (M.from_f2(b)[0] + rng.randrange(0, 2) * P, M.from_f2(b)[1] + rng.randrange(0, 4) * P)
+        assert M.to_f2(M.m2(A, Bb)) == B.f2mul(a, b)
+        assert M.to_f2(M.s2(A, 6)) == B.f2mul(a, a)
+    for v in (0, 1, P - 1, P, 2 * P - 1, 2 ** 392 - 1, 2519 * P, rng.randrange(2 ** 392)):
+        assert M.red(v) % P == v % P
+
+
+def test_g2_point_formulas_match_oracle():
+    rng = random.Random(5)
+    pts = [g2_point(rng) for _ in range(4)] + [g2_point(rng, False) for _ in range(2)]
+    for pt in pts:
+        q = g2_point(rng)
+        # doubling chains, mixed and Jacobian additions, the bounds carried through many steps
+        acc = (*enc(pt)[:2], M.ONE2, False)
+        ref = pt
+        for k in range(40):
+            acc = M.dbl(acc)
+            ref = B.ec_dbl(B.FP2, ref)
+            if k % 3 == 0:
+                acc = M.madd_fast(acc, *enc(q))
+                ref = B.ec_add(B.FP2, ref, q)
+            if k % 5 == 0:
+                acc = M.jadd(acc, jac(q, rng))
+                ref = B.ec_add(B.FP2, ref, q)
+            if k % 7 == 0:
+                acc = M.jadd_fast(jac(pt, rng), acc)
+                ref = B.ec_add(B.FP2, ref, pt)
+        assert M.to_affine(acc) == ref
+
+
+def bucket_run(run, affine, rng):
+    """k_msm_bucket28 for G2 on the model: fast formulas, Z tested once, exact recomputation when poisoned"""
+    def pts():
+        for pt, neg in run:
+            if affine:
+                x, y = enc(pt)
+                yield (x, M.neg2(y) if neg else y)
+            else:
+                X, Y, Z, _ = jac(pt, rng)
+                yield (X, M.neg2(Y) if neg else Y, Z, False)
+    acc = M.inf()
+    for q in pts():
+        acc = M.madd_fast(acc, *q) if affine else M.jadd_fast(acc, q)
+    if not M.poisoned(acc):
+        return acc, False
+    acc = M.inf()
+    for q in pts():
+        acc = M.madd(acc, *q) if affine else M.jadd(acc, q)
+    return acc, True
+
+
+def test_g2_msm_bucket_runs():
+    rng = random.Random(9)
+    p = [g2_point(rng) for _ in range(5)]
+
+    def osum(run):
+        acc = None
+        for pt, neg in run:
+            acc = B.ec_add(B.FP2, acc, B.ec_neg(B.FP2, pt) if neg else pt)
+        return acc
+
+    normal = [[(p[k % 5], rng.random() < 0.5) for k in rng.sample(range(30), 7)] for _ in range(3)]
+    exceptional = [[(p[0], False), (p[0], False)], [(p[1], False), (p[1], True), (p[2], False)],
+                   [(p[3], False), (p[4], False), (B.ec_add(B.FP2, p[3], p[4]), True)]]
+    for run in normal + exceptional:
+        for affine in (True, False):
+            got, pois = bucket_run(run, affine, rng)
+            assert M.to_affine(got) == osum(run)
+            assert pois == (run in exceptional) or run in normal and not pois
+
+
+def test_g2_subgroup_test_model():
+    """fp2_28.hpp g2_in_subgroup28: psi(P) == -[|u|] P on the lazy form, against r P == O"""
+    rng = random.Random(11)
+    cases = [g2_point(rng) for _ in range(2)] + [g2_point(rng, False) for _ in range(2)]
+    tors = B.ec_mul(B.FP2, g2_point(rng, False), M1.r)  # an h2-torsion point
+    cases.append(B.ec_add(B.FP2, g2_point(rng), tors))
+    for pt in cases:
+        want = B.ec_mul(B.FP2, pt, M1.r) is None
+        assert M.in_subgroup(pt) == want
