@@ -96,11 +96,14 @@ def cpu_baseline(scheme, pk, rounds, sigs, seconds):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ctypes as orc
     threads, affinity, quota, model = host_cores()
-    probe = max(threads, 16)
+    # probe with 4 rounds per thread (one round per thread mostly timed the threads' start-up), then size the
+    # sample so the timed run takes about `seconds`
+    probe = 4 * threads
     t0 = time.perf_counter()
     orc.verify_batch(scheme, pk, rounds[:probe], sigs[:probe], nthreads=threads)
     per = (time.perf_counter() - t0) / probe
     n = int(min(len(rounds), max(probe, seconds / max(per, 1e-9))))
+    n -= n % threads if n > threads else 0  # whole rounds per thread
     t0 = time.perf_counter()
     v, _ = orc.verify_batch(scheme, pk, rounds[:n], sigs[:n], nthreads=threads)
     dt = time.perf_counter() - t0

@@ -297,20 +297,22 @@ int make_seed(uint64_t seed, uint32_t words[8]) {
 }
 
 // MSM geometry for groups of gsize rounds; glv: the endomorphism split (2 x gsize points, 63-bit scalar halves)
+static bool window_ok(int sbits, int c) {
+  // keep the top window's t bits at >= c - 4, since each of its 2^(t-1) buckets collects ~m / 2^(t-1) entries
+  // and a bucket that spans many chunks is summed serially by k_msm_bucket_fix (127-bit scalars at c = 14 would
+  // leave t = 1: two buckets holding the whole set)
+  const int nw = (sbits + 1 + c - 1) / c, t = sbits - c * (nw - 1);
+  return t >= c - 4;
+}
 dh::msm_geom geom_for(size_t gsize, bool glv = false) {
   const size_t npts = glv ? 2 * gsize : gsize;
   const int sbits = glv ? 63 : 127;  // scalar bits (k_scalars)
   int lg = 0;
   while (((size_t)1 << (lg + 1)) <= npts) lg++;
   int c = std::max(3, std::min(16, lg - 2));
-  // keep the top window's t bits at >= c - 4, since each of its 2^(t-1) buckets collects ~m / 2^(t-1) entries
-  // and a bucket that spans many chunks is summed serially by k_msm_bucket_fix (127-bit scalars at c = 14 would
-  // leave t = 1: two buckets holding the whole set)
-  while (c > 3) {
-    const int nw = (sbits + 1 + c - 1) / c, t = sbits - c * (nw - 1);
-    if (t >= c - 4) break;
-    c--;
-  }
+  // c = lg(npts) - 2 (a 131k-round shard keeps c = 16: a cost model trading bucket-pass additions against the
+  // reduction picked c = 13 there and measured 8.5 ms against 6.7, gpurun_out r03g)
+  while (c > 3 && !window_ok(sbits, c)) c--;
   dh::msm_geom g;
   g.gsize = (uint32_t)gsize;
   g.c = c;

@@ -194,6 +194,41 @@ __device__ __constant__ uint32_t PSI_Y28[2][14] = {
      0xa544de3u, 0x556a044u, 0x9c66da5u, 0x38ec515u, 0x000cea3u}};
 DH_DEV f228 f2_c28(const uint32_t (*c)[14]) { return {f28_c(c[0]), f28_c(c[1])}; }
 
+// psi^2 constants (Fp: the c1 parts are 0)
+__device__ __constant__ uint32_t PSI2_X28[14] = {0x2421b59u, 0xbee4867u, 0x1d31002u, 0x4760184u, 0x4cc5086u, 0xc76dc00u, 0xaae891bu,
+                                                 0xac70ad2u, 0xfe377c4u, 0xe4686b8u, 0x5ed1568u, 0x8f5a180u, 0x02b5c1fu, 0x000d1a4u};
+__device__ __constant__ uint32_t PSI2_Y28[14] = {0xcb7adf3u, 0x26fffffu, 0x3fd4ea0u, 0xf320443u, 0x9b20bcbu, 0x1d54a7eu, 0xf2fca33u,
+                                                 0x19759edu, 0xac6b042u, 0x39151c5u, 0x691dcb4u, 0xe56da35u, 0xb903c85u, 0x0014896u};
+DH_DEV j228 j228_neg(const j228& p) { return {p.x, f2_neg3(p.y), p.z, p.inf}; }  // Y < 3 stays a valid coordinate
+DH_DEV j228 j228_psi(const j228& p) {  // (conj(X) PSI_X, conj(Y) PSI_Y, conj(Z)), Z < 12
+  return {f2_red(f2_mul(f2_conj(p.x), f2_c28(PSI_X28))), f2_red(f2_mul(f2_conj(p.y), f2_c28(PSI_Y28))),
+          {p.z.c0, f28_lin<12>(p.z.c1, -1, p.z.c1, 0)}, p.inf};
+}
+DH_DEV j228 j228_psi2(const j228& p) {
+  const f28 cx = f28_c(PSI2_X28), cy = f28_c(PSI2_Y28);
+  return {{f28_mul(p.x.c0, cx), f28_mul(p.x.c1, cx)}, {f28_mul(p.y.c0, cy), f28_mul(p.y.c1, cy)}, p.z, p.inf};
+}
+DH_DEV j228 j228_mul_uabs(const j228& p) {  // [|u|] P, Jacobian base
+  j228 acc = p;
+#pragma unroll 1
+  for (int b = 62; b >= 0; b--) {
+    acc = j228_dbl(acc);
+    if ((cst::U_ABS >> b) & 1) acc = j228_add<true>(acc, p);
+  }
+  return acc;
+}
+// clear_cofactor(G2) = [h_eff] P by the endomorphism method of RFC 9380 Appendix G.3, the steps of h2c.hpp
+// h2c_clear_g2 on the lazy form (tests/fp2_28_model.py clear): the G2 group check's and the leaves' hash side
+DH_DEV jac<fp2> g2_clear28(const jac<fp2>& q) {
+  j228 p{f2_from_fp2(q.x), f2_from_fp2(q.y), f2_from_fp2(q.z), fp2_is_zero(q.z)};
+  const j228 t1 = j228_neg(j228_mul_uabs(p));
+  j228 t3 = j228_add<true>(j228_psi2(j228_dbl(p)), j228_neg(j228_psi(p)));
+  const j228 t2 = j228_neg(j228_mul_uabs(j228_add<true>(t1, j228_psi(p))));
+  t3 = j228_add<true>(j228_add<true>(j228_add<true>(t3, t2), j228_neg(t1)), j228_neg(p));
+  if (t3.inf) return jac_inf<fp2>();
+  return {f2_to_fp2(t3.x), f2_to_fp2(t3.y), f2_to_fp2(t3.z)};
+}
+
 // G2 subgroup test of an affine point (codec.hpp g2_in_subgroup, same algorithm): psi(P) == [u] P = -[|u|] P,
 // |u| = 0xd201000000010000, on the lazy form (tests/fp2_28_model.py in_subgroup). ld() returns P (12 x 32 form); it is
 // called where P's coordinates are needed (the loop's five mixed additions, the final comparison), so a caller that

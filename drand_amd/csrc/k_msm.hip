@@ -503,6 +503,7 @@ DH_DEV void set_zero(f228& z) {
 // the lazy-form curve of each signature group: element / point types and the formulas the MSM needs
 struct c28_g1 {
   static constexpr int OCC = 2;  // waves per SIMD the bucket pass is compiled for
+  static constexpr size_t LCAP = 32;  // longest bucket-pass chunk
   using E = f28;
   using P = j28;
   using F = fp;  // 12 x 32-bit form of the outputs
@@ -539,6 +540,7 @@ struct c28_g1 {
 };
 struct c28_g2 {
   static constexpr int OCC = 1;  // 512 registers: the G2 mixed addition's values fit VGPRs + AGPRs, no scratch
+  static constexpr size_t LCAP = 64;
   using E = f228;
   using P = j228;
   using F = fp2;
@@ -890,7 +892,8 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
   uint32_t* bB = ws.buckets + nk * jw;
   uint32_t* pB = ws.part + msm_nchunks(ws.max_entries) * 2 * jw;
   if (ws.max_entries) {
-    const uint32_t L = msm_chunk_len(ws.max_entries);
+    // chunks of up to LCAP entries (G2: 64, so half as many keys cut by chunk boundaries for k_msm_bucket_fix28)
+    const uint32_t L = msm_chunk_len(ws.max_entries, C::LCAP);
     const size_t nch = (ws.max_entries + L - 1) / L;
     hipLaunchKernelGGL((k_msm_bucket28<C, true>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, S, ws.buckets,
                        ws.part, ws.meta, skip, g.half_stride);

@@ -40,9 +40,9 @@ struct msm_ws {
 };
 
 // balanced bucket accumulation: entries per chunk, and workspace sizes for `max_entries` list entries
-inline uint32_t msm_chunk_len(size_t max_entries) {
+inline uint32_t msm_chunk_len(size_t max_entries, size_t cap = 32) {
   size_t L = max_entries / 262144;
-  return (uint32_t)(L < 4 ? 4 : L > 32 ? 32 : L);
+  return (uint32_t)(L < 4 ? 4 : L > cap ? cap : L);
 }
 inline size_t msm_nchunks(size_t max_entries) { return max_entries / msm_chunk_len(max_entries) + 2; }
 inline size_t msm_part_bytes(size_t max_entries, size_t jac_words, int nsets) {

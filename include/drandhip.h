@@ -75,8 +75,8 @@ int dh_key_len(int scheme);
  *   rand_out     n*32 bytes SHA-256(sig) (RandomnessFromSignature) or NULL
  *   seed         0 = draw the random-linear-combination seed from the OS CSPRNG; otherwise deterministic
  * One call runs on one internal stream by default (its per-round kernels, then its MSM and pairing checks on a
- * high-priority stream): a 4M-round call runs at 92% of the rate of 8 concurrent 1M calls, a 1M-round call at
- * 81% (its ~16 ms latency tail is exposed). DRANDHIP_SPLIT="chunk,workers" / dh_set_split cut a call into
+ * high-priority stream): a 4M-round call runs at ~94% of the rate of 8 concurrent 1M calls, a 1M-round call at
+ * ~85% (its ~8 ms latency tail, MSM + pairing check, is exposed). DRANDHIP_SPLIT="chunk,workers" / dh_set_split cut a call into
  * chunks verified on several streams instead.
  * Returns DH_OK or a negative error code (no verdicts are valid on error).
  */

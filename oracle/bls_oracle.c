@@ -18,7 +18,7 @@
  *   mock chain generator pattern      /root/reference/client/test/result/mock/result.go:84-127
  *
  * Pinned by the reference KATs /root/reference/crypto/schemes_test.go:81-130 and
- * /root/reference/crypto/curve_test.go:10-31 (tests/test_oracle_kat.py), and cross-checked
+ * /root/reference/crypto/curve_test.go:10-31 (tests/test_oracle.py, KATs in tests/kat.py), and cross-checked
  * against the independent pure-Python model oracle/bls_py.py.
  *
  * Build: see oracle/Makefile (gcc -O3 -shared -fPIC -pthread).

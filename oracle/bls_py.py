@@ -16,7 +16,7 @@ optimal-ate pairing over |u| = 0xd201000000010000.
 
 Pinned by: /root/reference/crypto/schemes_test.go:81-130 (TestVerifyBeacon, 4 beacons)
 and /root/reference/crypto/curve_test.go:10-31 (TestBLS12381Compatv112) — see
-tests/test_oracle_kat.py.
+tests/test_oracle.py (KATs in tests/kat.py).
 """
 import hashlib
 

@@ -218,3 +218,52 @@ def in_subgroup(pt):
     if not zero2(lin2(3, 3, m2(px, z2), 1, X, -1)):  # psi(P).x Z^2 == X
         return False
     return zero2(add2(m2(py, z3), Y))               # psi(P).y Z^3 == -Y
+
+
+# ---- cofactor clearing [h_eff] P (fp2_28.hpp g2_clear28, RFC 9380 G.3 as h2c.hpp h2c_clear_g2)
+def _psi2_consts():
+    import bls_py as B
+    xi = (1, 1)
+    cx = B.f2inv(B.f2pow(xi, (p * p - 1) // 3))
+    cy = B.f2inv(B.f2pow(xi, (p * p - 1) // 2))
+    assert cx[1] == 0 and cy[1] == 0
+    return cx[0], cy[0]
+
+
+def jneg(P):
+    X, Y, Z, fl = P
+    return (X, (lin(3, Y[0], -1, Y[0], 0), lin(3, Y[1], -1, Y[1], 0)), Z, fl)
+
+
+def psi_jac(P):
+    cx, cy = _psi_consts()
+    X, Y, Z, fl = P
+    return (red2(m2(conj2(X), from_f2(cx))), red2(m2(conj2(Y), from_f2(cy))), (Z[0], lin(12, Z[1], -1, Z[1], 0)), fl)
+
+
+def psi2_jac(P):
+    cx, cy = _psi2_consts()
+    X, Y, Z, fl = P
+    fx, fy = M.from_fp(cx), M.from_fp(cy)
+    return ((mont(X[0], fx), mont(X[1], fx)), (mont(Y[0], fy), mont(Y[1], fy)), Z, fl)
+
+
+def mul_uabs(P):
+    acc = P
+    for b in range(62, -1, -1):
+        acc = dbl(acc)
+        if (M.U >> b) & 1:
+            acc = jadd(acc, P)
+    return acc
+
+
+def clear(P):
+    t1 = jneg(mul_uabs(P))
+    t2 = psi_jac(P)
+    t3 = psi2_jac(dbl(P))
+    t3 = jadd(t3, jneg(t2))
+    t2 = jadd(t1, t2)
+    t2 = jneg(mul_uabs(t2))
+    t3 = jadd(t3, t2)
+    t3 = jadd(t3, jneg(t1))
+    return jadd(t3, jneg(P))

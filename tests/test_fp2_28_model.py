@@ -11,7 +11,6 @@ import fp28_model as M1
 import fp2_28_model as M
 
 P = M.p
-H2 = 0x5d543a95414e7f1091d50792876a202cd91de4547085abaa68a205b2e5a7ddfa628f1cb4d9e82ef21537e293a6691ae1616ec6e786f0c70cf1c38e31c7238e5
 
 
 def rng_f2(rng):
@@ -124,3 +123,12 @@ def test_g2_subgroup_test_model():
     for pt in cases:
         want = B.ec_mul(B.FP2, pt, M1.r) is None
         assert M.in_subgroup(pt) == want
+
+
+def test_g2_cofactor_clearing_model():
+    """fp2_28.hpp g2_clear28 (RFC 9380 G.3 on the lazy form) equals [h_eff] P for random E2 points (off G2)"""
+    rng = random.Random(17)
+    for _ in range(2):
+        pt = g2_point(rng, False)
+        got = M.to_affine(M.clear(jac(pt, rng)))
+        assert got == B.ec_mul(B.FP2, pt, B.H_EFF_G2)
