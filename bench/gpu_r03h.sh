@@ -1,0 +1,21 @@
+#!/bin/bash
+# r03h: re-establish the round's evidence on the restored tree: GPU tests, headline bench, G2 unchained bench,
+# 131k-round shard, and the rocprofv3 kernel-trace summary of the headline command.
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p "$O"
+cd "$R"
+T=${1:-r03h}
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > "$O/gpu_tests_$T.log" 2>&1
+timeout -k 10 300 python bench.py > "$O/bench_$T.json" 2> "$O/bench_$T.err"
+timeout -k 10 300 python bench.py --scheme pedersen-bls-unchained --no-cpu-baseline --single-call-steps 0 > "$O/bench_unch_$T.json" 2> "$O/bench_unch_$T.err"
+timeout -k 10 300 python bench.py --total-rounds 131072 --no-cpu-baseline --single-call-steps 0 > "$O/shard131k_$T.json" 2> "$O/shard131k_$T.err"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$T" -o run --output-format csv -- \
+  python3 "$R/bench.py" --steps 8 --warmup 8 --single-call-steps 0 --no-cpu-baseline > "$O/prof_$T.log" 2>&1
+echo "done $T"
+cd "$R"
+DRANDHIP_LIB=$R/drand_amd/libdrandhip_count.so timeout -k 10 400 python -u bench/count_products.py --rounds 1048576 \
+  --out "$O/count_products_$T.json" > "$O/count_products_$T.log" 2>&1
+echo "count done $T"
