@@ -310,6 +310,13 @@ dh::msm_geom geom_for(size_t gsize, bool glv = false) {
   int lg = 0;
   while (((size_t)1 << (lg + 1)) <= npts) lg++;
   int c = std::max(3, std::min(16, lg - 2));
+  // DRANDHIP_MSM_C (experiments): the window width of batch-sized groups (>= 65,536 rounds)
+  static const int c_env = [] {
+    const char* e = getenv("DRANDHIP_MSM_C");
+    const int v = e ? atoi(e) : 0;
+    return v >= 4 && v <= 16 ? v : 0;
+  }();
+  if (c_env && gsize >= 65536) c = c_env;
   // c = lg(npts) - 2 (a 131k-round shard keeps c = 16: a cost model trading bucket-pass additions against the
   // reduction picked c = 13 there and measured 8.5 ms against 6.7, gpurun_out r03g)
   while (c > 3 && !window_ok(sbits, c)) c--;

@@ -601,22 +601,28 @@ DH_DEV f28 c28_g1::endo_x(const f28& x) { return f28_mul(x, f28_c(BETA28)); }
 
 // The batch's points in the lazy affine form, each followed (index n + i) by its endomorphism image (phi on G1,
 // psi on G2): S from the decoded signatures; Q from the Jacobian hash points, made affine here with one
-// variable-time inversion per PREP28_K rounds (Montgomery's trick: the prefix products of Z go to Q's x slots on the
+// variable-time inversion per K rounds (Montgomery's trick: the prefix products of Z go to Q's x slots on the
 // way forward, each 1/Z comes out on the way back). The bucket pass then takes mixed additions for both point sets:
 // 7M + 4S per entry instead of 11M + 5S for the hash points, against ~8 (G1) / ~25 (G2) products per round here. A
 // hash point at infinity (Z = 0, probability ~2^-255) cannot be the message of a valid signature: its round is
-// marked DEC_BAD, which is its VerifyBeacon verdict.
-constexpr uint32_t PREP28_K = 16;
+// marked DEC_BAD, which is its VerifyBeacon verdict. K (rounds per inversion) follows the batch size so that the
+// launch fills the chip's 2-wave residency (131,072 lanes): 8 at 1M rounds, 1 at a 131k shard (prep28_k).
+constexpr uint32_t PREP28_KMAX = 16;
+static uint32_t prep28_k(size_t n) {
+  uint32_t k = 1;
+  while (k < PREP28_KMAX && n / (2 * k) >= 131072) k *= 2;
+  return k;
+}
 template <class C>
-__global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint8_t* __restrict__ status, const uint32_t* __restrict__ sig_aff,
-                                                       const uint32_t* __restrict__ q_pts, uint32_t* __restrict__ S,
-                                                       uint32_t* __restrict__ Q) {
+__global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint32_t K, uint8_t* __restrict__ status,
+                                                       const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ q_pts,
+                                                       uint32_t* __restrict__ S, uint32_t* __restrict__ Q) {
   using E = typename C::E;
   using F = typename C::F;
   constexpr int EW = C::EW, FW = npw<F>::N;
-  const size_t lo = gtid() * PREP28_K;
+  const size_t lo = gtid() * K;
   if (lo >= n) return;
-  const size_t hi = min(n, lo + PREP28_K);
+  const size_t hi = min(n, lo + K);
 #pragma unroll 1
   for (size_t i = lo; i < hi; i++) {
     if (status[i] != DEC_OK) continue;
@@ -878,9 +884,10 @@ __global__ __launch_bounds__(64) void k_msm_windows28(const uint32_t* __restrict
 hipError_t launch_msm_prep28(int sig_g2, size_t n, uint8_t* status, const uint32_t* sig_aff, const uint32_t* q_pts,
                              uint32_t* S, uint32_t* Q, hipStream_t st) {
   if (!n) return hipSuccess;
-  const size_t nt = (n + PREP28_K - 1) / PREP28_K;
-  if (sig_g2) hipLaunchKernelGGL(k_msm_prep28<c28_g2>, dim3(nblk(nt, 256)), dim3(256), 0, st, n, status, sig_aff, q_pts, S, Q);
-  else hipLaunchKernelGGL(k_msm_prep28<c28_g1>, dim3(nblk(nt, 256)), dim3(256), 0, st, n, status, sig_aff, q_pts, S, Q);
+  const uint32_t K = prep28_k(n);
+  const size_t nt = (n + K - 1) / K;
+  if (sig_g2) hipLaunchKernelGGL(k_msm_prep28<c28_g2>, dim3(nblk(nt, 256)), dim3(256), 0, st, n, K, status, sig_aff, q_pts, S, Q);
+  else hipLaunchKernelGGL(k_msm_prep28<c28_g1>, dim3(nblk(nt, 256)), dim3(256), 0, st, n, K, status, sig_aff, q_pts, S, Q);
   return hipGetLastError();
 }
 

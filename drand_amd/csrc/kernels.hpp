@@ -1,5 +1,6 @@
 // Host-side declarations of the kernel launchers in kernels.hip (internal to libdrandhip).
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -41,8 +42,15 @@ struct msm_ws {
 
 // balanced bucket accumulation: entries per chunk, and workspace sizes for `max_entries` list entries
 inline uint32_t msm_chunk_len(size_t max_entries, size_t cap = 32) {
+  // DRANDHIP_MSM_LMIN (experiments): the shortest chunk (default 4)
+  static const size_t lmin = [] {
+    const char* e = getenv("DRANDHIP_MSM_LMIN");
+    const long v = e ? atol(e) : 0;
+    return (size_t)(v >= 1 && v <= 64 ? v : 4);
+  }();
   size_t L = max_entries / 262144;
-  return (uint32_t)(L < 4 ? 4 : L > cap ? cap : L);
+  if (L < lmin) L = lmin;
+  return (uint32_t)(L > cap ? cap : L);
 }
 inline size_t msm_nchunks(size_t max_entries) { return max_entries / msm_chunk_len(max_entries) + 2; }
 inline size_t msm_part_bytes(size_t max_entries, size_t jac_words, int nsets) {
