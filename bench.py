@@ -59,6 +59,8 @@ def parse():
                          "the bench already keeps --streams calls in flight)")
     ap.add_argument("--node-check", choices=["auto", "on", "off"], default="auto",
                     help="node-wide RLC check with an all-gather of partial sums (auto: when N > 1)")
+    ap.add_argument("--hw-queues", type=int, default=16,
+                    help="GPU_MAX_HW_QUEUES for this process (0: keep the environment's)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse N ranks on one GPU with host-staged collectives")
     return ap.parse_args()
@@ -120,6 +122,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ["DRANDHIP_SPLIT"] = args.split  # the library's default one-call split, read when it loads
+    # 16 hardware queues per process instead of the 4 the environment sets: with 8 batches in flight (16 library
+    # streams), a batch's latency-bound tail (MSM reduction, pairing check) no longer holds up another batch's
+    # per-round kernels queued behind it on a shared queue (131k-round shard 19.0 -> 20.7 M/s, profiles/r03j); HIP
+    # reads it when it initialises, below
+    if args.hw_queues > 0:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
     import torch.distributed as dist
     from drand_amd import _lib, scheme_from_name
@@ -330,7 +338,7 @@ def main():
         "node_roofline_basis": "executed kernel work %d M/beacon (prep_sig + prep_msg + MSM, bench/workmodel.json "
                                "executed_M_per_beacon) at the measured peak" % wm["executed_M_per_beacon"][ex_key],
         "verdicts_ok": ok,
-        "streams": S, "warmup_batches": warm_batches,
+        "streams": S, "warmup_batches": warm_batches, "hip_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
         "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in prof.items()},
         "stages_ms_single_stream": {k: round(v["total_ms"] / max(1, v["count"]), 3) for k, v in prof1.items()},
         "single_call": single,

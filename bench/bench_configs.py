@@ -32,6 +32,9 @@ sys.path.insert(0, os.path.join(ROOT, "bench"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 R_ORDER = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
 
+# as bench.py: 16 hardware queues per process, so one batch's latency-bound tail does not block the others
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("DRANDHIP_BENCH_HW_QUEUES", "16")
+
 
 def secret(name):
     return (int.from_bytes(hashlib.sha256(b"drandhip-sk-" + name.encode()).digest(), "big") % R_ORDER).to_bytes(32, "big")
