@@ -899,8 +899,9 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
   uint32_t* bB = ws.buckets + nk * jw;
   uint32_t* pB = ws.part + msm_nchunks(ws.max_entries) * 2 * jw;
   if (ws.max_entries) {
-    // chunks of up to LCAP entries (G2: 64, so half as many keys cut by chunk boundaries for k_msm_bucket_fix28)
-    const uint32_t L = msm_chunk_len(ws.max_entries, C::LCAP);
+    // chunks of up to LCAP entries (G2: 64, so half as many keys cut by chunk boundaries for k_msm_bucket_fix28),
+    // about two per lane the chip holds at the pass's occupancy (G1 2 waves/SIMD: 262,144 chunks; G2 1: 131,072)
+    const uint32_t L = msm_chunk_len(ws.max_entries, C::LCAP, (size_t)C::OCC * 131072);
     const size_t nch = (ws.max_entries + L - 1) / L;
     hipLaunchKernelGGL((k_msm_bucket28<C, true>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, S, ws.buckets,
                        ws.part, ws.meta, skip, g.half_stride);

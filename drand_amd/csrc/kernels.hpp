@@ -41,7 +41,7 @@ struct msm_ws {
 };
 
 // balanced bucket accumulation: entries per chunk, and workspace sizes for `max_entries` list entries
-inline uint32_t msm_chunk_len(size_t max_entries, size_t cap = 32) {
+inline uint32_t msm_chunk_len(size_t max_entries, size_t cap = 32, size_t target_chunks = 262144) {
   // the shortest chunk: 8 entries (a 131k-round shard at c = 16 holds ~8 entries per bucket, so shorter chunks cut
   // most buckets and leave their sums to k_msm_bucket_fix: 4 -> 8 took the shard's MSM from 2.75 to 2.42 ms,
   // profiles/r03k); DRANDHIP_MSM_LMIN overrides it for experiments
@@ -50,7 +50,7 @@ inline uint32_t msm_chunk_len(size_t max_entries, size_t cap = 32) {
     const long v = e ? atol(e) : 0;
     return (size_t)(v >= 1 && v <= 64 ? v : 8);
   }();
-  size_t L = max_entries / 262144;
+  size_t L = max_entries / target_chunks;
   if (L < lmin) L = lmin;
   return (uint32_t)(L > cap ? cap : L);
 }
