@@ -296,7 +296,8 @@ int make_seed(uint64_t seed, uint32_t words[8]) {
   return DH_OK;
 }
 
-// MSM geometry for groups of gsize rounds; glv: the endomorphism split (2 x gsize points, 63-bit scalar halves)
+// MSM geometry for groups of gsize rounds; parts: 1 = 127-bit scalars, 2 = the endomorphism split (2 x gsize points,
+// 63-bit scalar halves), 4 = the G2 psi split (4 x gsize points, 31-bit scalar parts)
 static bool window_ok(int sbits, int c) {
   // keep the top window's t bits at >= c - 4, since each of its 2^(t-1) buckets collects ~m / 2^(t-1) entries
   // and a bucket that spans many chunks is summed serially by k_msm_bucket_fix (127-bit scalars at c = 14 would
@@ -304,9 +305,9 @@ static bool window_ok(int sbits, int c) {
   const int nw = (sbits + 1 + c - 1) / c, t = sbits - c * (nw - 1);
   return t >= c - 4;
 }
-dh::msm_geom geom_for(size_t gsize, bool glv = false) {
-  const size_t npts = glv ? 2 * gsize : gsize;
-  const int sbits = glv ? 63 : 127;  // scalar bits (k_scalars)
+dh::msm_geom geom_for(size_t gsize, int parts = 1) {
+  const size_t npts = (size_t)parts * gsize;
+  const int sbits = parts == 4 ? 31 : parts == 2 ? 63 : 127;  // scalar bits (k_scalars)
   int lg = 0;
   while (((size_t)1 << (lg + 1)) <= npts) lg++;
   int c = std::max(3, std::min(16, lg - 2));
@@ -330,7 +331,7 @@ dh::msm_geom geom_for(size_t gsize, bool glv = false) {
   uint32_t nseg = std::max(1u, std::min(8192u, g.nbuck / 8));
   g.nseg = nseg;
   g.seglen = (g.nbuck - 1 + nseg - 1) / nseg;
-  g.halves = glv ? 2 : 1;
+  g.halves = (uint32_t)parts;
   g.half_stride = 0;  // set by the caller: the point-array offset of the endomorphism images
   return g;
 }
@@ -489,7 +490,7 @@ static const std::vector<size_t>& fixed_ladder() {
 // level observed (faulty groups -> -ln(1 - f) faults per group, at least one per failing group; when every
 // group failed, 5 per group). The next size minimises the expected cost of the rest of the descent.
 static double msm_cost_ms(double m, size_t g) {
-  const dh::msm_geom gg = geom_for(g, true);
+  const dh::msm_geom gg = geom_for(g, 2);
   return 9.0 + 1.8e-6 * m * (double)(gg.nwin * gg.halves) / 2.0;  // fitted on 127-bit entries (8 per round at c = 16)
 }
 static double check_cost_ms(double groups) { return 12.0 + 0.0025 * groups; }
@@ -575,13 +576,15 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (sig_stride < (size_t)sig_len || sig_stride % 4) return fail(DH_EINVAL, "bad signature stride %zu", sig_stride);
   if (stats) memset(stats, 0, 4 * sizeof(uint64_t));
   if (n == 0) return DH_OK;
-  // sorted-list entries keep a sign bit and address 2n points (the endomorphism images follow the n points)
-  if (n >= 0x40000000u) return fail(DH_EINVAL, "batch too large");
+  // the MSM runs on lazily reduced 28-bit points (k_msm.hip MSM28), whose workspace points take 48 (G1) / 96 (G2)
+  // words; DRANDHIP_MSM32=1 selects the 12 x 32-bit MSM kept as the second implementation. G2 on the 28-bit MSM
+  // splits each scalar in four psi parts, otherwise in two endomorphism halves.
+  const bool msm28 = !msm32_selected();
+  const int parts = g2 && msm28 ? 4 : 2;
+  // sorted-list entries keep a sign bit and address parts * n points (the endomorphism images follow the n points)
+  if (n >= ((size_t)1 << 31) / parts) return fail(DH_EINVAL, "batch too large");
   const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
   const size_t aw = jw * 2 / 3;
-  // the MSM runs on lazily reduced 28-bit points (k_msm.hip MSM28), whose workspace points take 48 (G1) / 96 (G2)
-  // words; DRANDHIP_MSM32=1 selects the 12 x 32-bit MSM kept as the second implementation
-  const bool msm28 = !msm32_selected();
   const size_t wsw = msm28 ? (g2 ? 96 : 48) : jw;
 
   timed_launches T(st);
@@ -623,9 +626,9 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     if (presorted) {
       hipStream_t ts = w->tail;
       HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, ts));
-      HIP_TRY(dh::launch_scalars(d_seed, n, nullptr, w->scal.as<uint4>(), 1, ts));
+      HIP_TRY(dh::launch_scalars(d_seed, n, nullptr, w->scal.as<uint4>(), parts, ts));
       HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, ts));
-      g0 = geom_for(n, true);
+      g0 = geom_for(n, parts);
       g0.half_stride = (uint32_t)n;
       rc = msm_workspace(w, g0, n, 1, wsw, ws0);
       if (rc) return rc;
@@ -645,11 +648,11 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     }));
     if (!presorted) {
       HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
-      HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), 1, st));
+      HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), parts, st));
     }
     if (msm28) {
-      HIP_TRY(w->s28.ensure(2 * n * (g2 ? 64 : 32) * 4));
-      HIP_TRY(w->q28.ensure(2 * n * (g2 ? 64 : 32) * 4));
+      HIP_TRY(w->s28.ensure(parts * n * (g2 ? 64 : 32) * 4));
+      HIP_TRY(w->q28.ensure(parts * n * (g2 ? 64 : 32) * 4));
       HIP_TRY(T.run(g2 ? "k_msm_prep28<fp2>" : "k_msm_prep28<fp>", [&] {
         return dh::launch_msm_prep28(g2, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
                                      w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), st);
@@ -705,7 +708,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   }
   while (m > 0 && gsize > 1) {
     gsize = std::min(gsize, m);
-    dh::msm_geom g = geom_for(gsize, true);
+    dh::msm_geom g = geom_for(gsize, parts);
     g.half_stride = (uint32_t)n;
     const size_t ngroups = (m + gsize - 1) / gsize;
     const bool pre = level == 0 && presorted;

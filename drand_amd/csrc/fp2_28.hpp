@@ -233,15 +233,24 @@ DH_DEV jac<fp2> g2_clear28(const jac<fp2>& q) {
 // |u| = 0xd201000000010000, on the lazy form (tests/fp2_28_model.py in_subgroup). ld() returns P (12 x 32 form); it is
 // called where P's coordinates are needed (the loop's five mixed additions, the final comparison), so a caller that
 // keeps P in memory (k_sub_sig_g2) holds no copy of it in registers across the doublings.
-template <class LD>
-DH_DEV bool g2_in_subgroup28(LD ld) {
-  auto q = [&](int k) { const aff<fp2> a = ld(); return f2_from_fp2(k ? a.y : a.x); };
+// [|u|] P on the lazy form; EXACT = false takes the mixed additions without their exceptional-case tests (the MSM's
+// fast formulas): an exceptional case (acc = +-P, or a 2-torsion doubling) leaves Z = 0 mod p, which every later step
+// keeps, so a poisoned result (Z = 0 without the infinity flag) is recomputed with the exact formulas
+template <bool EXACT, class Q>
+DH_DEV j228 g2_mul_uabs_ld(Q q) {
   j228 acc{q(0), q(1), f2_one(), false};
 #pragma unroll 1
   for (int b = 62; b >= 0; b--) {
     acc = j228_dbl(acc);
-    if ((cst::U_ABS >> b) & 1) acc = j228_madd_ld<true>(acc, q);
+    if ((cst::U_ABS >> b) & 1) acc = j228_madd_ld<EXACT>(acc, q);
   }
+  return acc;
+}
+template <class LD>
+DH_DEV bool g2_in_subgroup28(LD ld) {
+  auto q = [&](int k) { const aff<fp2> a = ld(); return f2_from_fp2(k ? a.y : a.x); };
+  j228 acc = g2_mul_uabs_ld<false>(q);
+  if (j228_poisoned(acc)) acc = g2_mul_uabs_ld<true>(q);
   if (acc.inf) return false;  // psi(P) is finite
   const f228 z2 = f2_sqr<12>(acc.z);
   const f228 px = f2_mul(f2_conj(q(0)), f2_c28(PSI_X28));               // (4, 6)

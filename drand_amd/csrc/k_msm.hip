@@ -36,11 +36,15 @@ DH_DEV int32_t signed_digit(const uint4& s, int w, const msm_geom& g, uint32_t& 
 // grp ? grp[e] : e / gsize. The sorted list stores point indices (| NEG_BIT for a negative digit), bucket by bucket.
 DH_DEV size_t entry_group(const uint32_t* grp, size_t e, uint32_t gsize) { return grp ? grp[e] : e / gsize; }
 
-// the scalar of half h of an entry: the whole 127-bit scalar, or with the endomorphism split a = (x, y), b = (z, w)
+// the scalar of half h of an entry: the whole 127-bit scalar, or with the endomorphism split a = (x, y), b = (z, w),
+// or with the G2 psi split the 31-bit part in word h
 DH_DEV uint4 half_scalar(const uint4& s, uint32_t h, const msm_geom& g) {
   if (g.halves == 1) return s;
+  if (g.halves == 4) return make_uint4(h == 0 ? s.x : h == 1 ? s.y : h == 2 ? s.z : s.w, 0, 0, 0);
   return h ? make_uint4(s.z, s.w, 0, 0) : make_uint4(s.x, s.y, 0, 0);
 }
+// the round of a point index: the endomorphism images follow the n points (parts of half_stride = nround points)
+DH_DEV uint32_t round_of(uint32_t idx, uint32_t nround) { return idx < nround ? idx : idx % nround; }
 
 __global__ void k_msm_hist(const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ sidx,
                            const uint32_t* __restrict__ grp, size_t m, const uint4* __restrict__ scal, msm_geom g,
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket(const uint32_t* _
     const uint32_t raw = list[j];
     const uint32_t idx = raw & ~NEG_BIT;
     const bool neg = (raw & NEG_BIT) != 0;
-    if (!skip || skip[idx < nround ? idx : idx - nround] == DEC_OK) {
+    if (!skip || skip[round_of(idx, nround)] == DEC_OK) {
       if constexpr (AFFINE) {
         aff<F> pt = ld_aff_aos<F>(pts, idx);
         pt.y = f_select(neg, f_neg(pt.y), pt.y);
@@ -503,6 +507,7 @@ DH_DEV void set_zero(f228& z) {
 // the lazy-form curve of each signature group: element / point types and the formulas the MSM needs
 struct c28_g1 {
   static constexpr int OCC = 2;  // waves per SIMD the bucket pass is compiled for
+  static constexpr int PARTS = 2;  // P, phi(P): two 63-bit scalar halves
   static constexpr size_t LCAP = 32;  // longest bucket-pass chunk
   using E = f28;
   using P = j28;
@@ -540,6 +545,7 @@ struct c28_g1 {
 };
 struct c28_g2 {
   static constexpr int OCC = 1;  // 512 registers: the G2 mixed addition's values fit VGPRs + AGPRs, no scratch
+  static constexpr int PARTS = 4;  // P, psi(P), psi^2(P), psi^3(P): four 31-bit scalar parts
   static constexpr size_t LCAP = 64;
   using E = f228;
   using P = j228;
@@ -571,6 +577,9 @@ struct c28_g2 {
   // psi(x, y) = (conj(x) PSI_X, conj(y) PSI_Y), reduced back to < 2
   DH_DEV static E endo_x(const E& x) { return f2_red(f2_mul(f2_conj(x), f2_c28(PSI_X28))); }
   DH_DEV static E endo_y(const E& y) { return f2_red(f2_mul(f2_conj(y), f2_c28(PSI_Y28))); }
+  // psi^2(x, y) = (x PSI2_X, y PSI2_Y) with constants in Fp
+  DH_DEV static E psi2_x(const E& x) { return f2_red({f28_mul(x.c0, f28_c(PSI2_X28)), f28_mul(x.c1, f28_c(PSI2_X28))}); }
+  DH_DEV static E psi2_y(const E& y) { return f2_red({f28_mul(y.c0, f28_c(PSI2_Y28)), f28_mul(y.c1, f28_c(PSI2_Y28))}); }
 };
 
 template <class C>
@@ -600,7 +609,7 @@ __device__ __constant__ uint32_t BETA28[14] = {0xa75929au, 0x681b798u, 0x22a3e9d
 DH_DEV f28 c28_g1::endo_x(const f28& x) { return f28_mul(x, f28_c(BETA28)); }
 
 // The batch's points in the lazy affine form, each followed (index n + i) by its endomorphism image (phi on G1,
-// psi on G2): S from the decoded signatures; Q from the Jacobian hash points, made affine here with one
+// psi on G2; G2 also psi^2 and psi^3 at 2n + i and 3n + i, the four parts of its scalars): S from the decoded signatures; Q from the Jacobian hash points, made affine here with one
 // variable-time inversion per K rounds (Montgomery's trick: the prefix products of Z go to Q's x slots on the
 // way forward, each 1/Z comes out on the way back). The bucket pass then takes mixed additions for both point sets:
 // 7M + 4S per entry instead of 11M + 5S for the hash points, against ~8 (G1) / ~25 (G2) products per round here. A
@@ -608,6 +617,20 @@ DH_DEV f28 c28_g1::endo_x(const f28& x) { return f28_mul(x, f28_c(BETA28)); }
 // marked DEC_BAD, which is its VerifyBeacon verdict. K (rounds per inversion) follows the batch size so that the
 // launch fills the chip's 2-wave residency (131,072 lanes): 8 at 1M rounds, 1 at a 131k shard (prep28_k).
 constexpr uint32_t PREP28_KMAX = 16;
+// the endomorphism images of affine point i at part * n + i
+template <class C>
+DH_DEV void prep28_images(uint32_t* __restrict__ out, size_t n, size_t i, const typename C::E& x, const typename C::E& y) {
+  constexpr int EW = C::EW;
+  st28(out + 2 * EW * (n + i), C::endo_x(x), 0);
+  st28(out + 2 * EW * (n + i) + EW, C::endo_y(y), 0);
+  if constexpr (C::PARTS == 4) {
+    const typename C::E x2 = C::psi2_x(x), y2 = C::psi2_y(y);
+    st28(out + 2 * EW * (2 * n + i), x2, 0);
+    st28(out + 2 * EW * (2 * n + i) + EW, y2, 0);
+    st28(out + 2 * EW * (3 * n + i), C::endo_x(x2), 0);
+    st28(out + 2 * EW * (3 * n + i) + EW, C::endo_y(y2), 0);
+  }
+}
 static uint32_t prep28_k(size_t n) {
   uint32_t k = 1;
   while (k < PREP28_KMAX && n / (2 * k) >= 131072) k *= 2;
@@ -630,8 +653,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint32_t K, uin
     const E x = C::in(a.x), y = C::in(a.y);
     st28(S + 2 * EW * i, x, 0);
     st28(S + 2 * EW * i + EW, y, 0);
-    st28(S + 2 * EW * (n + i), C::endo_x(x), 0);
-    st28(S + 2 * EW * (n + i) + EW, C::endo_y(y), 0);
+    prep28_images<C>(S, n, i, x, y);
   }
   E acc = C::one();
   bool any = false;
@@ -663,8 +685,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint32_t K, uin
     const E y = C::mulr(C::in(q.y), C::mulr(zi2, zi));
     st28(Q + 2 * EW * k, x, 0);
     st28(Q + 2 * EW * k + EW, y, 0);
-    st28(Q + 2 * EW * (n + k), C::endo_x(x), 0);
-    st28(Q + 2 * EW * (n + k) + EW, C::endo_y(y), 0);
+    prep28_images<C>(Q, n, k, x, y);
   }
 }
 
@@ -713,7 +734,7 @@ __global__ __launch_bounds__(256, C::OCC) void k_msm_bucket28(const uint32_t* __
   for (uint32_t j = (uint32_t)s; j < e; j++) {
     const uint32_t raw = list[j];
     const uint32_t idx = raw & ~NEG_BIT;
-    if (!skip || skip[idx < nround ? idx : idx - nround] == DEC_OK) acc = bucket_add<C, AFFINE>(acc, pts, raw, false);
+    if (!skip || skip[round_of(idx, nround)] == DEC_OK) acc = bucket_add<C, AFFINE>(acc, pts, raw, false);
     const bool ends = j + 1 == kend;
     if (ends || j + 1 == e) {
       if (C::poisoned(acc)) {  // an exceptional case somewhere in the run: again with the exact formulas
@@ -722,7 +743,7 @@ __global__ __launch_bounds__(256, C::OCC) void k_msm_bucket28(const uint32_t* __
         for (uint32_t k = run0; k <= j; k++) {
           const uint32_t r2 = list[k];
           const uint32_t i2 = r2 & ~NEG_BIT;
-          if (!skip || skip[i2 < nround ? i2 : i2 - nround] == DEC_OK) acc = bucket_add<C, AFFINE>(acc, pts, r2, true);
+          if (!skip || skip[round_of(i2, nround)] == DEC_OK) acc = bucket_add<C, AFFINE>(acc, pts, r2, true);
         }
       }
       if (first && starts_before) {

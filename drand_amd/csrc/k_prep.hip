@@ -152,7 +152,7 @@ __global__ __launch_bounds__(EXC_THREADS, 1) void k_add_iso_g2_exc(const uint32_
 // ---------------------------------------------------------------- RLC scalars
 // r_i = first 16 bytes of SHA-256(seed[32] || i_be64), 0 for rounds that failed decoding.
 __global__ __launch_bounds__(256) void k_scalars(const uint32_t* __restrict__ seed_words, size_t n,
-                                                 const uint8_t* __restrict__ status, int glv, uint4* __restrict__ scal) {
+                                                 const uint8_t* __restrict__ status, int parts, uint4* __restrict__ scal) {
   size_t i = gtid();
   if (i >= n) return;
   uint32_t w[16];
@@ -169,9 +169,12 @@ __global__ __launch_bounds__(256) void k_scalars(const uint32_t* __restrict__ se
   // little-endian words of a 127-bit integer (top bit cleared: the MSM's signed window digits need one spare
   // bit; the batch check's soundness error is 2^-127 per group), or with the endomorphism split two 63-bit
   // halves a, b: the round's scalar is a + b*mu mod r (mu = the endomorphism's eigenvalue, -z^2 on G1 or z on
-  // G2, |mu| > 2^63, so distinct (a, b) give distinct scalars: soundness error 2^-126 per group)
-  uint4 r = glv ? make_uint4(s.h[3], s.h[2] & 0x7fffffffu, s.h[1], s.h[0] & 0x7fffffffu)
-                : make_uint4(s.h[3], s.h[2], s.h[1], s.h[0] & 0x7fffffffu);
+  // G2, |mu| > 2^63, so distinct (a, b) give distinct scalars: soundness error 2^-126 per group), or on G2 four
+  // 31-bit parts a, b, c, d: the scalar a + b z + c z^2 + d z^3 (psi = [z] on G2), |value| < 2^31 (1 + 2^64 +
+  // 2^128 + 2^192) < r / 2, so distinct parts give distinct scalars: soundness error 2^-124 per group
+  uint4 r = parts == 4   ? make_uint4(s.h[3] & 0x7fffffffu, s.h[2] & 0x7fffffffu, s.h[1] & 0x7fffffffu, s.h[0] & 0x7fffffffu)
+            : parts == 2 ? make_uint4(s.h[3], s.h[2] & 0x7fffffffu, s.h[1], s.h[0] & 0x7fffffffu)
+                         : make_uint4(s.h[3], s.h[2], s.h[1], s.h[0] & 0x7fffffffu);
   if (status && status[i] != DEC_OK) r = make_uint4(0, 0, 0, 0);
   scal[i] = r;
 }
@@ -232,9 +235,9 @@ hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n,
 }
 
 
-hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, int glv, hipStream_t st) {
+hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, int parts, hipStream_t st) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_scalars, dim3(nblk(n, 256)), dim3(256), 0, st, seed_words, n, status, glv, scal);
+  hipLaunchKernelGGL(k_scalars, dim3(nblk(n, 256)), dim3(256), 0, st, seed_words, n, status, parts, scal);
   return hipGetLastError();
 }
 

@@ -13,6 +13,8 @@ namespace dh {
 // Scalars: 127-bit integers (halves = 1), or with the endomorphism split (halves = 2) a pair (a, b) of 63-bit
 // integers in one uint4 (x, y = a; z, w = b): entry e then stands for two points, P_e with scalar a and
 // endo(P_e) (stored half_stride points further on) with scalar b, i.e. P_e with the scalar a + b*mu mod r.
+// G2 (halves = 4): four 31-bit parts (x, y, z, w) for P_e, psi(P_e), psi^2(P_e), psi^3(P_e) (part h at h * half_stride
+// points on), i.e. the scalar a + b z + c z^2 + d z^3 (psi = [z] on G2).
 struct msm_geom {
   uint32_t gsize;
   int c;
@@ -20,8 +22,8 @@ struct msm_geom {
   uint32_t nbuck;
   uint32_t nseg;
   uint32_t seglen;
-  uint32_t halves;       // 1, or 2 for the endomorphism split
-  uint32_t half_stride;  // point index offset of endo(P) (halves = 2)
+  uint32_t halves;       // 1; 2 for the endomorphism split; 4 for the G2 psi split
+  uint32_t half_stride;  // point index offset of endo(P) (halves = 2) / of each psi power (halves = 4)
 };
 inline size_t msm_entries(const msm_geom& g, size_t m) { return m * (size_t)g.nwin * g.halves; }
 
@@ -70,7 +72,8 @@ hipError_t launch_hash(int sig_g2, const uint64_t* rounds, const uint8_t* prevs,
                        hipStream_t st);
 // RLC scalars from SHA-256(seed || i): 127-bit (glv = 0) or a pair of 63-bit halves (glv = 1, msm_geom.halves = 2);
 // 0 for rounds whose status is not DEC_OK (status null: every round gets its scalar)
-hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, int glv, hipStream_t st);
+// parts: 1 = one 127-bit scalar, 2 = two 63-bit halves, 4 = four 31-bit parts (msm_geom halves)
+hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, int parts, hipStream_t st);
 // endomorphism images for the split MSM: sig_aff[n + i] = endo(sig_aff[i]), q_pts[n + i] = endo(q_pts[i])
 // (G1: phi(x, y) = (beta x, y); G2: psi), so the sorted lists address them as point n + i
 hipError_t launch_endo(int sig_g2, size_t n, uint32_t* sig_aff, uint32_t* q_pts, hipStream_t st);

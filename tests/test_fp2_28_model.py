@@ -132,3 +132,36 @@ def test_g2_cofactor_clearing_model():
         pt = g2_point(rng, False)
         got = M.to_affine(M.clear(jac(pt, rng)))
         assert got == B.ec_mul(B.FP2, pt, B.H_EFF_G2)
+
+
+def test_g2_psi_split_scalars():
+    """The G2 MSM's four-part scalars (k_scalars parts = 4, k_msm_prep28<c28_g2> images): with psi = [z] on G2,
+    a P + b psi(P) + c psi^2(P) + d psi^3(P) = [a + b z + c z^2 + d z^3] P for signatures (in G2), and after the
+    group check's cofactor clearing the same holds for the uncleared hash points ([h] commutes with psi). The images
+    are formed as the prep kernel forms them (psi affine with conj and PSI_X / PSI_Y, psi^2 with the Fp constants,
+    psi^3 = psi(psi^2)), and 31-bit parts give distinct scalars (|value| < r / 2)."""
+    rng = random.Random(23)
+    z = -M1.U  # the BLS parameter (negative)
+    r = M1.r
+    bound = (2 ** 31 - 1) * (1 + abs(z) + z * z + abs(z) ** 3)
+    assert 2 * bound < r
+
+    def images(pt):
+        P0 = (*enc(pt), M.ONE2, False)
+        P1 = M.psi_jac(P0)
+        P2 = M.psi2_jac(P0)
+        P3 = M.psi_jac(P2)
+        return [M.to_affine(Q) for Q in (P0, P1, P2, P3)]
+
+    for subgroup in (True, False):
+        for _ in range(2):
+            pt = g2_point(rng, subgroup)
+            parts = [rng.randrange(2 ** 31) for _ in range(4)]
+            acc = None
+            for k, im in enumerate(images(pt)):
+                acc = B.ec_add(B.FP2, acc, B.ec_mul(B.FP2, im, parts[k]))
+            s = sum(parts[k] * z ** k for k in range(4))
+            if subgroup:
+                assert acc == B.ec_mul(B.FP2, pt, s % r)
+            else:
+                assert B.ec_mul(B.FP2, acc, B.H_EFF_G2) == B.ec_mul(B.FP2, B.ec_mul(B.FP2, pt, B.H_EFF_G2), s % r)
