@@ -240,6 +240,35 @@ __global__ __launch_bounds__(64) void k_partial_leaf(const uint32_t* __restrict_
 // them. One lane per round left most of the chip idle at 10^4-10^5 rounds and ran 33 terms x 127 additions
 // serially; four lanes cut the per-round latency ~3.8x for ~6% more doublings.
 constexpr int LG_LANES = 4, LG_MAXK = 9;  // terms per lane and pass (t <= 36: one pass)
+// G2: the chain on the lazily reduced 28-bit form (fp2_28.hpp), the MSM's fast mixed additions (no exceptional-case
+// tests); a chain that met an exceptional case ends with Z = 0 mod p and is run again with the exact 32-bit formulas
+template <bool EXACT>
+DH_DEV j228 lagrange_chain28(const uint32_t* __restrict__ L, int q, int c0, int nc, const uint32_t* __restrict__ sig_aff,
+                             const uint32_t* idx, uint32_t* lp, uint32_t* ln) {
+  j228 acc = j228_inf();
+#pragma unroll 1
+  for (int b = 255; b >= 0; b--) {
+    if ((b & 31) == 31)
+      for (int i = 0; i < nc; i++) {
+        const uint32_t* Lk = L + (size_t)(q + LG_LANES * (c0 + i)) * 16;
+        lp[i] = Lk[b >> 5];
+        ln[i] = Lk[8 + (b >> 5)];
+      }
+    acc = j228_dbl(acc);
+#pragma unroll 1
+    for (int i = 0; i < nc; i++) {
+      const uint32_t pb = (lp[i] >> (b & 31)) & 1, nb = (ln[i] >> (b & 31)) & 1;
+      if (pb | nb) {
+        const aff<fp2> pt = ld_aff_aos<fp2>(sig_aff, idx[i]);
+        const f228 x = f2_from_fp2(pt.x);
+        f228 y = f2_from_fp2(pt.y);
+        if (nb) y = f2_neg3(y);
+        acc = j228_madd<EXACT>(acc, x, y);
+      }
+    }
+  }
+  return acc;
+}
 template <class F>
 __global__ __launch_bounds__(64) void k_lagrange(const uint32_t* __restrict__ sel, const uint32_t* __restrict__ lam,
                                                  const uint32_t* __restrict__ lam_set, const uint8_t* __restrict__ ok,
@@ -262,8 +291,16 @@ __global__ __launch_bounds__(64) void k_lagrange(const uint32_t* __restrict__ se
     uint32_t* ln = lnS[threadIdx.x];
     for (int c0 = 0; c0 < nt; c0 += LG_MAXK) {  // more than LG_MAXK terms: several passes
       const int nc = nt - c0 < LG_MAXK ? nt - c0 : LG_MAXK;
-      jac<F> part_acc = jac_inf<F>();
       for (int i = 0; i < nc; i++) idx[i] = S[q + LG_LANES * (c0 + i)];
+      if constexpr (sizeof(F) == sizeof(fp2)) {
+        // a poisoned chain (an exceptional case met by the fast additions) is recomputed by the exact 32-bit chain below
+        const j228 a28 = lagrange_chain28<false>(L, q, c0, nc, sig_aff, idx, lp, ln);
+        if (!j228_poisoned(a28)) {
+          if (!a28.inf) acc = jac_add(acc, jac<F>{f2_to_fp2(a28.x), f2_to_fp2(a28.y), f2_to_fp2(a28.z)});
+          continue;
+        }
+      }
+      jac<F> part_acc = jac_inf<F>();
       for (int b = 255; b >= 0; b--) {
         if ((b & 31) == 31)
           for (int i = 0; i < nc; i++) {
