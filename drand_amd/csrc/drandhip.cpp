@@ -114,6 +114,9 @@ struct worker {
   size_t cached_key_len = 0;
   int cached_key_g2 = -1;
   uint8_t cached_key_ok = 0;
+  // fault density (faults per round) the last bisection of this worker observed at its first level: a replay's
+  // consecutive windows fail alike, so a dense one starts its next bisection with smaller groups (next_group_size)
+  double fault_density = 0;
   void release_all() {
     dbuf* all[] = {&s28, &q28, &entries_alt, &cflags, &crank, &cscan, &status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &h2c_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
@@ -512,10 +515,18 @@ static double descent_cost(double m, double d, size_t gprev, size_t* best) {
   return c_best;
 }
 
-static size_t next_group_size(size_t gsize, size_t ngroups, size_t nfail, size_t m_prev, size_t m_next) {
+static size_t next_group_size(size_t gsize, size_t ngroups, size_t nfail, size_t m_prev, size_t m_next, double hint) {
   // level 0 (one group) says only that some round is bad: 1024 costs about what 4096 does over 1M rounds and
-  // its groups still pass at a 0.1% fault density (4096-round groups then all fail)
-  if (gsize == m_prev && m_prev > 4096) return 1024;
+  // its groups still pass at a 0.1% fault density (4096-round groups then all fail). When the worker's previous
+  // bisection saw dense faults (> 1 per 2000 rounds: most 1024-groups fail), 256-round groups first: the ladder
+  // sweep on a 0.2%-faulty chained window put 256-first ladders 5-9% ahead of 1024-first ones
+  // (profiles/bisect_sweep_r03s.txt)
+  const bool dense = hint > 1.0 / 2000;
+  if (gsize == m_prev && m_prev > 4096) return dense ? 256 : 1024;
+  // ... and continues 256 -> 32 -> 4 -> per-round leaves, the best ladder of that sweep (231.7 ms per 1M window
+  // against 240-259 for the others); the cost model below was fitted on sparser failures
+  if (dense && (gsize == 256 || gsize == 32)) return gsize == 256 ? 32 : 4;
+  if (dense && gsize == 4) return 1;
   const double f = (double)nfail / (double)ngroups;
   const double per_group = nfail == ngroups ? 5.0 : -std::log1p(-f);
   const double faults = std::max((double)nfail, per_group * (double)ngroups);
@@ -762,6 +773,11 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     level++;
     const size_t nfail = nfail32;
     if (stats) stats[1] += nfail;
+    if (level == 1 && nfail == 0) w->fault_density = 0;  // a clean batch clears the density hint
+    if (level == 2) {  // the first bisection level's failure rate: the density hint of the worker's next batch
+      const double f = (double)nfail / (double)ngroups;
+      w->fault_density = (f >= 1.0 ? 5.0 : -std::log1p(-f)) / (double)gsize;
+    }
     if (nfail == 0) {
       m = 0;
       break;
@@ -769,7 +785,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     std::swap(w->entries, w->entries_alt);
     const size_t m_prev = m;
     m = nfail * gsize - (last_pass ? 0 : ngroups * gsize - m_prev);  // only the last group may be short
-    gsize = fixed.empty() ? next_group_size(gsize, ngroups, nfail, m_prev, m)
+    gsize = fixed.empty() ? next_group_size(gsize, ngroups, nfail, m_prev, m, w->fault_density)
                           : (size_t)(level - 1 < (int)fixed.size() ? fixed[level - 1] : 1);
   }
   if (m > 0) {

@@ -129,6 +129,34 @@ DH_DEV f28 f28_add(const f28& a, const f28& b) { return f28_lin<0>(a, 1, b, 1); 
 template <int K>
 DH_DEV f28 f28_sub(const f28& a, const f28& b) { return f28_lin<K>(a, 1, b, -1); }
 DH_DEV f28 f28_scale(const f28& a, int c) { return f28_lin<0>(a, c, a, 0); }
+
+// Operands that feed only a product skip the carry pass. fp_mul28.hpp accumulates a column of 14 limb products plus
+// 14 quotient-digit products and the carry-in in 64 bits: with one operand's limbs < 2^29.6 and the other's < 2^29 a
+// column stays below 14 * 2^58.6 + 14 * 2^56 + 2^36 < 2^63, so limbs need not be normalised there (the value, which
+// the bounds are about, is the same integer). a + b limb by limb: limbs < 2^29.
+DH_DEV f28 f28_add_nc(const f28& a, const f28& b) {
+  f28 r;
+#pragma unroll
+  for (int i = 0; i < 14; i++) r.l[i] = a.l[i] + b.l[i];
+  return r;
+}
+// a + K p - b limb by limb, K p in a redundant form (limb 0 + 2^28, limbs 1..12 + 2^28 - 1, limb 13 - 1: the same
+// value) so that every limb is >= 0 given normalised a, b and b's top limb below K p's (b < (K - 1) p suffices);
+// limbs < 2^29.6
+template <int K>
+DH_DEV f28 f28_sub_nc(const f28& a, const f28& b) {
+  f28 r;
+  r.l[0] = a.l[0] + kp_limb<K>(0) + (1u << 28) - b.l[0];
+#pragma unroll
+  for (int i = 1; i < 13; i++) r.l[i] = a.l[i] + kp_limb<K>(i) + ((1u << 28) - 1) - b.l[i];
+  r.l[13] = a.l[13] + kp_limb<K>(13) - 1 - b.l[13];
+  return r;
+}
+// the smallest K' > K with a K' p constant (kp_limb): f28_sub_nc<kp_above(K)> takes any b < K p
+constexpr int kp_above(int K) {
+  return K < 3 ? 3 : K < 4 ? 4 : K < 6 ? 6 : K < 7 ? 7 : K < 8 ? 8 : K < 9 ? 9 : K < 12 ? 12 : K < 16 ? 16 : K < 18 ? 18
+       : K < 21 ? 21 : K < 24 ? 24 : K < 26 ? 26 : K < 32 ? 32 : 48;
+}
 DH_DEV f28 f28_one() {  // R' mod p
   const uint32_t k[14] = {0x347fcb8u, 0xd800000u, 0x002b119u, 0x0cde6d2u, 0xc7212e0u, 0x83a2090u, 0x037669fu,
                           0xda0f73eu, 0x9b09b42u, 0x1297bb0u, 0x515d98fu, 0x012ca7cu, 0x659fcfau, 0x000577au};

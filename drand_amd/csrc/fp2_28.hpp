@@ -51,17 +51,23 @@ DH_DEV f228 f2_red(const f228& a) { return {f28_red(a.c0), f28_red(a.c1)}; }
 DH_DEV f228 f2_neg3(const f228& a) { return {f28_lin<3>(a.c0, -1, a.c0, 0), f28_lin<3>(a.c1, -1, a.c1, 0)}; }
 DH_DEV f228 f2_conj(const f228& a) { return {a.c0, f28_lin<2>(a.c1, -1, a.c1, 0)}; }  // a1 < 2
 
-// Karatsuba: (a0 b0 - a1 b1 + 2p, (a0 + a1)(b0 + b1) - a0 b0 - a1 b1 + 4p) -> (4, 6)
+// Karatsuba: (a0 b0 - a1 b1 + 2p, (a0 + a1)(b0 + b1) - a0 b0 - a1 b1 + 4p) -> (4, 6). NC: the sums a0 + a1, b0 + b1
+// feed only the third product and keep their limbs unnormalised (f28_add_nc): fewer instructions, but the
+// independent limb sums lengthen live ranges, which the register-starved MSM reduction kernels pay for in scratch
+// (G2 MSM 15.8 -> 17.8 ms with NC everywhere); the subgroup test's doubling chain gains (k_sub_sig_g2 -3%)
+template <bool NC = false>
 DH_DEV f228 f2_mul(const f228& a, const f228& b) {
   const f28 t0 = f28_mul(a.c0, b.c0);
   const f28 t1 = f28_mul(a.c1, b.c1);
-  const f28 t2 = f28_mul(f28_add(a.c0, a.c1), f28_add(b.c0, b.c1));
+  const f28 t2 = NC ? f28_mul(f28_add_nc(a.c0, a.c1), f28_add_nc(b.c0, b.c1)) : f28_mul(f28_add(a.c0, a.c1), f28_add(b.c0, b.c1));
   return {f28_lin<2>(t0, 1, t1, -1), f28_lin3<4>(t2, 1, t0, -1, t1, -1)};
 }
-// complex squaring ((a0 + a1)(a0 - a1 + K p), 2 a0 a1), K >= a1's bound -> (2, 4)
-template <int K>
+// complex squaring ((a0 + a1)(a0 - a1 + K p), 2 a0 a1), K >= a1's bound -> (2, 4). NC (as f2_mul): both operands of
+// the first product skip the carry pass, the difference with K' = kp_above(K) (it needs a1 below (K' - 1) p)
+template <int K, bool NC = false>
 DH_DEV f228 f2_sqr(const f228& a) {
-  const f28 t0 = f28_mul(f28_add(a.c0, a.c1), f28_lin<K>(a.c0, 1, a.c1, -1));
+  const f28 t0 = NC ? f28_mul(f28_add_nc(a.c0, a.c1), f28_sub_nc<kp_above(K)>(a.c0, a.c1))
+                    : f28_mul(f28_add(a.c0, a.c1), f28_lin<K>(a.c0, 1, a.c1, -1));
   const f28 t1 = f28_mul(a.c0, a.c1);
   return {t0, f28_scale(t1, 2)};
 }
@@ -93,18 +99,19 @@ DH_DEV j228 j228_inf() {
 // The formulas are written in the order that keeps the fewest Fp2 values live (an Fp2 value is 28 VGPRs and every
 // product call clobbers 46 fixed registers): each intermediate dies as early as the formula allows.
 // dbl-2009-l (a = 0): X, Y < 2, Z < 12 -> (2, 2, 12)
+template <bool NC = false>
 DH_DEV j228 j228_dbl(const j228& p) {
   j228 r;
   r.inf = p.inf;
-  r.z = f2_scale(f2_mul(p.y, p.z), 2);                         // (8, 12)
-  const f228 b = f2_sqr<3>(p.y);                               // (2, 4)
-  const f228 c = f2_sqr<4>(b);                                 // (2, 4)
-  const f228 t = f2_sqr<7>(f2_add(p.x, b));                    // X + B < (5, 7)
-  const f228 a = f2_sqr<3>(p.x);                               // (2, 4)
+  r.z = f2_scale(f2_mul<NC>(p.y, p.z), 2);                     // (8, 12)
+  const f228 b = f2_sqr<3, NC>(p.y);                           // (2, 4)
+  const f228 c = f2_sqr<4, NC>(b);                             // (2, 4)
+  const f228 t = f2_sqr<7, NC>(f2_add(p.x, b));                // X + B < (5, 7)
+  const f228 a = f2_sqr<3, NC>(p.x);                           // (2, 4)
   const f228 d = f2_lin3<8, 16>(t, 2, a, -2, c, -2);           // (12, 24)
   const f228 e = f2_scale(a, 3);                               // (6, 12)
-  r.x = f2_red(f2_lin<24, 48>(f2_sqr<12>(e), 1, d, -2));       // (26, 52) -> < 2
-  const f228 m = f2_mul(e, f2_lin<3, 3>(d, 1, r.x, -1));       // e < 12, D - X3 + 3p < 27
+  r.x = f2_red(f2_lin<24, 48>(f2_sqr<12, NC>(e), 1, d, -2));   // (26, 52) -> < 2
+  const f228 m = f2_mul<NC>(e, f2_lin<3, 3>(d, 1, r.x, -1));   // e < 12, D - X3 + 3p < 27
   r.y = f2_red(f2_lin<16, 32>(m, 1, c, -8));                   // (20, 38) -> < 2
   return r;
 }
@@ -112,27 +119,27 @@ DH_DEV j228 j228_dbl(const j228& p) {
 // madd-2007-bl, q affine (< 3): P (2, 2, 12) -> (2, 2, 12). EXACT: the exceptional-case tests of curve.hpp
 // jac_add_aff. q's coordinates come from ldq(0) / ldq(1) at their single use, so they are never live across the
 // formula (the MSM reads them from memory there).
-template <bool EXACT, class LDQ>
+template <bool EXACT, bool NC = false, class LDQ>
 DH_DEV j228 j228_madd_ld(const j228& p, LDQ ldq) {
   if (p.inf) return j228{ldq(0), ldq(1), f2_one(), false};
-  const f228 z1z1 = f2_sqr<12>(p.z);                           // (2, 4)
-  const f228 rr = f2_lin<3, 3>(f2_mul(f2_mul(ldq(1), p.z), z1z1), 1, p.y, -1);  // S2 - Y1 + 3p: (7, 9)
-  const f228 h = f2_lin<3, 3>(f2_mul(ldq(0), z1z1), 1, p.x, -1);  // U2 - X1 + 3p: (7, 9)
+  const f228 z1z1 = f2_sqr<12, NC>(p.z);                       // (2, 4)
+  const f228 rr = f2_lin<3, 3>(f2_mul<NC>(f2_mul<NC>(ldq(1), p.z), z1z1), 1, p.y, -1);  // S2 - Y1 + 3p: (7, 9)
+  const f228 h = f2_lin<3, 3>(f2_mul<NC>(ldq(0), z1z1), 1, p.x, -1);  // U2 - X1 + 3p: (7, 9)
   if (EXACT && f2_zero(h)) {
-    if (f2_zero(rr)) return j228_dbl(p);
+    if (f2_zero(rr)) return j228_dbl<NC>(p);
     return j228_inf();
   }
-  const f228 hh = f2_sqr<9>(h);                                // (2, 4)
+  const f228 hh = f2_sqr<9, NC>(h);                            // (2, 4)
   j228 r;
   r.inf = false;
-  r.z = f2_lin3<4, 8>(f2_sqr<21>(f2_add(p.z, h)), 1, z1z1, -1, hh, -1);  // Z + H < 21 -> (6, 12)
+  r.z = f2_lin3<4, 8>(f2_sqr<21, NC>(f2_add(p.z, h)), 1, z1z1, -1, hh, -1);  // Z + H < 21 -> (6, 12)
   const f228 i = f2_scale(hh, 4);                              // (8, 16)
-  const f228 j = f2_mul(h, i);                                 // (4, 6)
-  const f228 v = f2_mul(p.x, i);                               // (4, 6)
+  const f228 j = f2_mul<NC>(h, i);                             // (4, 6)
+  const f228 v = f2_mul<NC>(p.x, i);                           // (4, 6)
   const f228 r2 = f2_scale(rr, 2);                             // (14, 18)
-  r.x = f2_red(f2_lin3<12, 18>(f2_sqr<18>(r2), 1, j, -1, v, -2));  // (14, 22) -> < 2
-  const f228 yj = f2_mul(p.y, j);                              // (4, 6)
-  const f228 m = f2_mul(r2, f2_lin<3, 3>(v, 1, r.x, -1));      // (4, 6)
+  r.x = f2_red(f2_lin3<12, 18>(f2_sqr<18, NC>(r2), 1, j, -1, v, -2));  // (14, 22) -> < 2
+  const f228 yj = f2_mul<NC>(p.y, j);                          // (4, 6)
+  const f228 m = f2_mul<NC>(r2, f2_lin<3, 3>(v, 1, r.x, -1));  // (4, 6)
   r.y = f2_red(f2_lin<8, 12>(m, 1, yj, -2));                   // (12, 18) -> < 2
   return r;
 }
@@ -241,8 +248,8 @@ DH_DEV j228 g2_mul_uabs_ld(Q q) {
   j228 acc{q(0), q(1), f2_one(), false};
 #pragma unroll 1
   for (int b = 62; b >= 0; b--) {
-    acc = j228_dbl(acc);
-    if ((cst::U_ABS >> b) & 1) acc = j228_madd_ld<EXACT>(acc, q);
+    acc = j228_dbl<true>(acc);
+    if ((cst::U_ABS >> b) & 1) acc = j228_madd_ld<EXACT, true>(acc, q);
   }
   return acc;
 }

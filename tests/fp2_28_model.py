@@ -56,9 +56,27 @@ def m2(a, b):
     return (lin(2, t0, 1, t1, -1), lin3(4, t2, 1, t0, -1, t1, -1))
 
 
+KP_AVAILABLE = (2, 3, 4, 6, 7, 8, 9, 12, 16, 18, 21, 24, 26, 32, 48)  # fp28.hpp DH_KP constants
+
+
+def kp_above(K):
+    """fp28.hpp kp_above: the smallest K' > K with a K' p constant"""
+    return min(k for k in KP_AVAILABLE if k > K)
+
+
+def sub_nc(K, a, b):
+    """fp28.hpp f28_sub_nc<K>: a + K p - b limb by limb with K p in a redundant form; every limb stays >= 0 when b's
+    top limb is below K p's (the value is the integer a + K p - b)"""
+    assert (b >> (28 * 13)) < ((K * p) >> (28 * 13)), "f28_sub_nc: b's top limb reaches K p's"
+    return lin(K, a, 1, b, -1)
+
+
 def s2(a, K):
-    """complex squaring ((a0 + a1)(a0 - a1 + K p), 2 a0 a1), K >= a1's bound: components < (2, 4)"""
-    t0 = mont(lin(0, a[0], 1, a[1], 1), lin(K, a[0], 1, a[1], -1))
+    """complex squaring ((a0 + a1)(a0 - a1 + K' p), 2 a0 a1), K >= a1's bound: components < (2, 4). Modelled in
+    the NC form (f2_sqr<K, true>: both product operands unnormalised, f28_add_nc / f28_sub_nc with K' = kp_above(K)),
+    whose product bound is the larger one; the plain form (K' = K, carries propagated) is bounded by it."""
+    assert a[1] < K * p, "f2_sqr<K>: a1 above K p"
+    t0 = mont(lin(0, a[0], 1, a[1], 1), sub_nc(kp_above(K), a[0], a[1]))
     t1 = mont(a[0], a[1])
     return (t0, lin(0, t1, 2, t1, 0))
 

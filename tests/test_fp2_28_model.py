@@ -165,3 +165,24 @@ def test_g2_psi_split_scalars():
                 assert acc == B.ec_mul(B.FP2, pt, s % r)
             else:
                 assert B.ec_mul(B.FP2, acc, B.H_EFF_G2) == B.ec_mul(B.FP2, B.ec_mul(B.FP2, pt, B.H_EFF_G2), s % r)
+
+
+def test_unnormalised_product_operands():
+    """fp28.hpp f28_add_nc / f28_sub_nc feed fp_mul28.hpp products with unnormalised limbs: every limb of the
+    redundant K p form keeps a + K p - b >= 0 limb by limb for normalised a, b (b's top limb below K p's), and a
+    product column (14 limb products of an add_nc and a sub_nc operand + 14 quotient-digit products + the carry-in)
+    stays below 2^64."""
+    mask = (1 << 28) - 1
+    max_sub = 0
+    for K in M.KP_AVAILABLE:
+        kp = [((K * P) >> (28 * i)) & mask for i in range(14)]
+        kp[13] = (K * P) >> (28 * 13)
+        red = [kp[0] + (1 << 28)] + [kp[i] + (1 << 28) - 1 for i in range(1, 13)] + [kp[13] - 1]
+        assert sum(v << (28 * i) for i, v in enumerate(red)) == K * P
+        for i in range(14):
+            lo = red[i] - (mask if i < 13 else kp[13] - 1)  # a_i = 0, b_i at its largest
+            assert lo >= 0, (K, i)
+            max_sub = max(max_sub, mask + red[i])
+    max_add = 2 * mask
+    column = 14 * max_add * max_sub + 14 * mask * mask + (1 << 36)
+    assert max_sub < 2 ** 29.6 and column < 2 ** 63
