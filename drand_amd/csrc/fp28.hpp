@@ -245,13 +245,14 @@ DH_DEV j28 j28_dbl(const j28& p) {
   const f28 a = sq(p.x);                                               // < 2
   const f28 b = sq(p.y);                                               // < 2
   const f28 c = sq(b);                                                 // < 2
-  const f28 t = sq(f28_add(p.x, b));                                   // (X + B)^2, X + B < 50
+  const f28 t = sq(INL ? f28_add_nc(p.x, b) : f28_add(p.x, b));       // (X + B)^2, X + B < 50
   const f28 d = f28_lin3<8>(t, 2, a, -2, c, -2);                       // D = 2 (T + 4p - A - C) < 12
   const f28 e = f28_scale(a, 3);                                       // E = 3A < 6
   const f28 f = sq(e);                                                 // < 2
   j28 r;
   r.x = f28_lin<24>(f, 1, d, -2);                                      // F + 24p - 2D < 26
-  const f28 m = mu(e, f28_sub<26>(d, r.x));                            // E (D + 26p - X3): 6 x 38 -> < 2
+  // E (D + 26p - X3): 6 x 38 -> < 2 (the carry-free form: D + 32p - X3, 6 x 44)
+  const f28 m = mu(e, INL ? f28_sub_nc<kp_above(26)>(d, r.x) : f28_sub<26>(d, r.x));
   r.y = f28_lin<16>(m, 1, c, -8);                                      // M + 16p - 8C < 18
   r.z = f28_scale(mu(p.y, p.z), 2);                                    // < 4
   r.inf = p.inf;

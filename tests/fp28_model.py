@@ -35,11 +35,18 @@ def zero(a): o=mont(a,1); return o==0 or o==p
 def from_fp(x): # x is the normal field element
     xr=x*R%p
     return mont(xr, pow(2,400,p))
+def sub_nc(K,a,b):
+    # fp28.hpp f28_sub_nc<K>: a + K p - b limb by limb (redundant K p); every limb stays >= 0 when b's top limb is
+    # below K p's
+    assert (b>>(28*13)) < ((K*p)>>(28*13)), "f28_sub_nc: b's top limb reaches K p's"
+    return lin(K,a,1,b,-1)
 def dbl(P):
+    # the subgroup test's inlined form (j28_dbl<true>): X + B and D + 32p - X3 feed their products carry-free
+    # (f28_add_nc, f28_sub_nc<kp_above(26)>); its product bound covers the out-of-line form's D + 26p - X3
     X,Y,Z,fl=P
     a=mont(X,X); b=mont(Y,Y); c=mont(b,b); t=mont(add(X,b),add(X,b))
     d=lin3(8,t,2,a,-2,c,-2); e=scale(a,3); f=mont(e,e)
-    x=lin(24,f,1,d,-2); m=mont(e,sub(26,d,x)); y=lin(16,m,1,c,-8); z=scale(mont(Y,Z),2)
+    x=lin(24,f,1,d,-2); m=mont(e,sub_nc(32,d,x)); y=lin(16,m,1,c,-8); z=scale(mont(Y,Z),2)
     return (x,y,z,fl)
 def inf(): return (ONE,ONE,0,True)
 def madd(P,qx,qy):
