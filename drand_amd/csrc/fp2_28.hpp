@@ -143,9 +143,9 @@ DH_DEV j228 j228_madd_ld(const j228& p, LDQ ldq) {
   r.y = f2_red(f2_lin<8, 12>(m, 1, yj, -2));                   // (12, 18) -> < 2
   return r;
 }
-template <bool EXACT>
+template <bool EXACT, bool NC = false>
 DH_DEV j228 j228_madd(const j228& p, const f228& qx, const f228& qy) {
-  return j228_madd_ld<EXACT>(p, [&](int k) { return k ? qy : qx; });
+  return j228_madd_ld<EXACT, NC>(p, [&](int k) { return k ? qy : qx; });
 }
 
 // add-2007-bl: (2, 2, 12) x (2, 2, 12) -> (2, 2, 6). EXACT as curve.hpp jac_add. q's coordinates come from ldq(k)

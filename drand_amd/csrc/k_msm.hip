@@ -552,7 +552,8 @@ struct c28_g2 {
   using F = fp2;
   static constexpr int EW = 2 * W28;
   DH_DEV static P inf() { return j228_inf(); }
-  DH_DEV static P madd_fast(const P& a, const E& x, const E& y) { return j228_madd<false>(a, x, y); }
+  // the bucket pass's additions take carry-free product operands (fp2_28.hpp NC); the reduction kernels' do not
+  DH_DEV static P madd_fast(const P& a, const E& x, const E& y) { return j228_madd<false, true>(a, x, y); }
   DH_DEV static P madd(const P& a, const E& x, const E& y) { return j228_madd<true>(a, x, y); }
   DH_DEV static P add_fast(const P& a, const P& b) { return j228_add<false>(a, b); }
   DH_DEV static P add(const P& a, const P& b) { return j228_add<true>(a, b); }
