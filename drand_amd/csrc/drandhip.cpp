@@ -1357,23 +1357,39 @@ int dh_check_partials(int scheme, const uint8_t* pk, size_t pk_len, const uint8_
   worker* w = L.w;
   int rc = set_device_and_stream(w);
   if (rc) return rc;
-  hipStream_t st = w->stream;
+  // the check is a batch's latency-bound tail: on the worker's high-priority stream, like verify_core's, so the other
+  // in-flight batches' per-round kernels do not hold back its one-wave pairing program
+  hipStream_t st = w->tail ? w->tail : w->stream;
   HIP_TRY(w->key_raw.ensure(96));
   HIP_TRY(w->key_aff.ensure(96 * 4));  // key + [h_eff] key (k_decode_key)
   HIP_TRY(w->key_ok.ensure(64));
   HIP_TRY(w->outA.ensure(jw * 4));
   HIP_TRY(w->outB.ensure(jw * 4));
   HIP_TRY(w->pass.ensure(16));
-  HIP_TRY(hipMemcpyAsync(w->key_raw.p, pk, pk_len, hipMemcpyHostToDevice, st));
-  HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(), w->key_ok.as<uint8_t>(), st));
-  w->cached_key_len = 0;  // key_aff is rewritten here: the batch path re-decodes its key on this worker
+  // the worker's decoded-key cache, as in verify_core: a chain's batches all check against one key, and decoding a G2
+  // key is a ~9.5 ms one-lane kernel that would sit on every node-wide check (and, had it evicted the cache, on the
+  // next batch of this worker too: the 131k-round per-rank shape ran at 12.5-14.9 M/s against 20.9 locally, r03y)
+  uint8_t key_ok = 0, pass = 0;
+  const bool key_hit = w->cached_key_len == pk_len && w->cached_key_g2 == (g2 ? 0 : 1) && !memcmp(w->cached_key, pk, pk_len);
+  if (key_hit) {
+    key_ok = w->cached_key_ok;
+  } else {
+    w->cached_key_len = 0;
+    HIP_TRY(hipMemcpyAsync(w->key_raw.p, pk, pk_len, hipMemcpyHostToDevice, st));
+    HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(), w->key_ok.as<uint8_t>(), st));
+    HIP_TRY(hipMemcpyAsync(&key_ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
+  }
   HIP_TRY(dh::launch_sum_partials(g2, (const uint32_t*)d_partials, k, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st));
   HIP_TRY(group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), 1, w->key_aff.as<uint32_t>(), w->pass.as<uint8_t>(), st,
                       w->key_aff.as<uint32_t>() + 48));
-  uint8_t key_ok = 0, pass = 0;
-  HIP_TRY(hipMemcpyAsync(&key_ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(&pass, w->pass.p, 1, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  if (!key_hit) {
+    memcpy(w->cached_key, pk, pk_len);
+    w->cached_key_len = pk_len;
+    w->cached_key_g2 = g2 ? 0 : 1;
+    w->cached_key_ok = key_ok;
+  }
   if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
   *pass_out = pass == 1 ? 1 : 0;
   return DH_OK;
