@@ -212,8 +212,13 @@ def verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, p
             raise RuntimeError(err or "node batch abandoned: dh_batch_begin failed on rank(s) %s" % bad)
         allp = gathered[:, :pb].contiguous().to(partials.device)
     try:
-        if allp.is_cuda:
-            torch.cuda.current_stream(allp.device).synchronize()  # the library reads it from its own streams
+        if world > 1 and allp.is_cuda:
+            # the gathered sums come from torch's stream and the library reads them from its own: wait for exactly
+            # that work (an event, not a whole-stream or device-wide wait that would also wait for the other
+            # in-flight batches); with one rank the sums are the library's own output, already complete
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(allp.device))
+            ev.synchronize()
         ok = ctypes.c_int(0)
         rc = lib.dh_check_partials(scheme.id, pk, len(pk), ptr(allp), world, ctypes.byref(ok))
         if rc != 0:
