@@ -15,4 +15,7 @@ for n in 131072 262144 524288; do
 done
 timeout -k 10 200 python bench.py --total-rounds 131072 $B > "$O/local_131072_$T.json" 2>> "$O/node_$T.err"
 timeout -k 10 200 python bench.py --total-rounds 131072 --node-check on $B > "$O/node_131072b_$T.json" 2>> "$O/node_$T.err"
+for S in 12 16; do
+  timeout -k 10 200 python bench.py --total-rounds 131072 --node-check on --streams $S $B > "$O/node_131072_s${S}_$T.json" 2>> "$O/node_$T.err"
+done
 echo "done $T"
