@@ -1,17 +1,21 @@
 #!/usr/bin/env python3
 """bench.py — verified beacons/sec on MI355X for the quicknet scheme (bls-unchained-g1-rfc9380).
 
-Workload (BASELINE.json configs[1] and the north_star's "1M-round quicknet chain"): batch-verify a 1M-round synthetic
-quicknet chain — G1 signatures, G2 group key, RFC 9380 hash-to-G1 — with per-round verdicts and SHA-256 randomness,
-inputs resident in HBM before the timed region. Strong scaling by default: the 1M rounds are split across the N
-GPUs of the node (rank r owns a contiguous shard), so N=8 is the north_star's 8xMI355X on a 1M-round chain;
---rounds-per-gpu gives weak scaling instead. One "step" = every rank verifies its shard once (one library call,
-fresh CSPRNG seed); with N > 1 each call runs under the node-wide check: the ranks' level-0 RLC sums are
-all-gathered over RCCL and ONE pairing check covers the node (drand_amd/dist.py). The verdict
-bitmaps are all-gathered at the end of the timed steps.
+Workload (BASELINE.json configs[1]): batch-verify a 1M-round synthetic quicknet chain per GPU — G1 signatures, G2
+group key, RFC 9380 hash-to-G1 — with per-round verdicts and SHA-256 randomness, inputs resident in HBM before the
+timed region. Weak scaling by default (rounds are independent objects): every rank owns its own
+contiguous 1M-round range of the chain, so N GPUs verify N x 1M rounds per step; --total-rounds n splits one n-round
+chain over the N GPUs instead (strong scaling, e.g. the north_star's 1M-round chain on 8 GPUs). One "step" = every
+rank verifies its rounds once (fresh CSPRNG seed); with N > 1 each batch runs under the node-wide check: the ranks'
+level-0 RLC sums are all-gathered over RCCL and ONE pairing check covers the node (drand_amd/dist.py), queued
+without a host wait; the verdict bitmaps are all-gathered at the end of the timed steps.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--total-rounds n | --rounds-per-gpu n] [--scheme name]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+`--gpus N` with N > 1 and no WORLD_SIZE in the environment launches the N ranks itself (a child
+`python -m torch.distributed.run`, started before this process touches the GPU) and exits with its status; rank 0's
+JSON line is the output. Under a launcher, WORLD_SIZE must equal --gpus.
 
 Rank 0 prints ONE JSON line: value = rounds verified by all ranks / max-over-ranks wall time of the K steps.
 "roofline": the dominant kernel's integer-multiply rate (its algorithmic mul32 per launch, bench/workmodel.json, over
@@ -21,10 +25,13 @@ bounded sample, on the host cores this process may use. "single_call": one dh_ve
 (the drop-in callers' shape), split by the library over its internal streams.
 """
 import argparse
+import collections
 import ctypes
 import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -41,8 +48,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--total-rounds", type=int, default=1 << 20, help="strong scaling: rounds split over the GPUs")
-    ap.add_argument("--rounds-per-gpu", type=int, default=0, help="weak scaling: rounds per GPU (overrides)")
+    ap.add_argument("--total-rounds", type=int, default=0,
+                    help="strong scaling: one chain of this many rounds split over the GPUs")
+    ap.add_argument("--rounds-per-gpu", type=int, default=0,
+                    help="weak scaling: rounds per GPU (default 1048576 when --total-rounds is not given)")
     ap.add_argument("--scheme", default="bls-unchained-g1-rfc9380")
     ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -53,7 +62,8 @@ def parse():
     ap.add_argument("--single-call-split", default="0,1", help="chunk rounds,workers of the one-call split (library "
                     "default: none)")
     ap.add_argument("--streams", type=int, default=8,
-                    help="batches in flight per GPU (host threads, each with its own HIP stream in libdrandhip)")
+                    help="batches in flight per GPU (local check: host threads, each with its own library worker; "
+                         "node-wide check: one host thread keeping this many batches queued)")
     ap.add_argument("--split", default="0",
                     help="one-call split inside the timed region ('chunk,workers'; 0 = each call on one stream: "
                          "the bench already keeps --streams calls in flight)")
@@ -116,11 +126,29 @@ def cpu_baseline(scheme, pk, rounds, sigs, seconds):
                       "hash + 2-pairing VerifyBeacon (CPU restatement, not kyber), %d threads, %.1f s" % (n, threads, dt)}
 
 
+def launch_ranks(args):
+    """--gpus N without a launcher: run this script as N ranks under torch.distributed.run (one process per GPU) in a
+    child process; this process never touches the GPU. Rank 0 prints the JSON line; the exit status is the child's."""
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("WORLD_SIZE=%d but --gpus %d: launch one rank per GPU" % (world, args.gpus))
     os.environ["DRANDHIP_SPLIT"] = args.split  # the library's default one-call split, read when it loads
     # 16 hardware queues per process instead of the 4 the environment sets: with 8 batches in flight (16 library
     # streams), a batch's latency-bound tail (MSM reduction, pairing check) no longer holds up another batch's
@@ -131,7 +159,7 @@ def main():
     import torch
     import torch.distributed as dist
     from drand_amd import _lib, scheme_from_name
-    from drand_amd.dist import gather_verdicts, pack_bits, shard_rounds, strong_shard, verify_node_batch
+    from drand_amd.dist import begin_node_batch, gather_verdicts, pack_bits, shard_rounds, strong_shard
 
     gloo = args.backend == "gloo"
     dev_index = 0 if gloo else local  # gloo rehearsal: every rank on GPU 0
@@ -149,10 +177,11 @@ def main():
     node_check = args.node_check == "on" or (args.node_check == "auto" and world > 1)
 
     sch = scheme_from_name(args.scheme)
-    weak = args.rounds_per_gpu > 0
+    weak = args.total_rounds <= 0
     if weak:
-        rounds = shard_rounds(rank, world, args.rounds_per_gpu)
-        total = world * args.rounds_per_gpu
+        per_gpu = args.rounds_per_gpu or (1 << 20)
+        rounds = shard_rounds(rank, world, per_gpu)
+        total = world * per_gpu
     else:
         rounds = strong_shard(rank, world, args.total_rounds)
         total = args.total_rounds
@@ -170,16 +199,10 @@ def main():
     d_rand = [torch.zeros((n, 32), dtype=torch.uint8, device=dev) for _ in range(S)]
     pbytes = lib.dh_partial_bytes(sch.id)
     d_part = [torch.zeros(pbytes, dtype=torch.uint8, device=dev) for _ in range(S)]
-    # one process group per in-flight slot: slot t on every rank issues its collectives in the same order
-    groups = [dist.new_group(list(range(world))) for _ in range(S)] if world > 1 and node_check else [None] * S
     torch.cuda.synchronize()
     state = {"node_check": node_check}
 
     def verify(slot):
-        if state["node_check"]:
-            verify_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot], d_rand[slot], d_part[slot], world,
-                              groups[slot], stage_host=gloo)
-            return
         rc = lib.dh_verify_batch_device(sch.id, pk, len(pk), ctypes.c_void_p(d_rounds.data_ptr()),
                                         ctypes.c_void_p(d_sigs.data_ptr()), sch.sig_len, None, 0, None, n,
                                         ctypes.c_void_p(d_verdict[slot].data_ptr()),
@@ -187,8 +210,35 @@ def main():
         if rc != 0:
             raise RuntimeError("dh_verify_batch_device: %s" % _lib.last_error())
 
+    def run_node_steps(k_steps, streams, gather=True):
+        """k_steps batches under the node-wide check, `streams` in flight, driven by ONE host thread: batch k is begun,
+        its record all-gathered and its check queued (no host wait under nccl), and the oldest batch is finished once
+        `streams` are queued. One thread issues every rank's collectives in the same order over one process group."""
+        pending = collections.deque()
+        bits = []
+
+        def retire():
+            slot, h = pending.popleft()
+            h.finish()
+            bits.append(pack_bits(d_verdict[slot]))
+
+        for k in range(k_steps):
+            if len(pending) == streams:
+                retire()
+            slot = k % streams
+            pending.append((slot, begin_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot], d_rand[slot],
+                                                   d_part[slot], world, None, stage_host=gloo, rank=rank)))
+        while pending:
+            retire()
+        if world > 1 and gather and k_steps:
+            b = torch.cat(bits)
+            gather_verdicts(b.cpu() if gloo else b, world)
+        torch.cuda.synchronize()
+
     def run_steps(k_steps, streams, gather=True):
         """k_steps batches, `streams` in flight: thread t runs steps t, t+streams, ... on its own output slot."""
+        if state["node_check"]:
+            return run_node_steps(k_steps, streams, gather)
         errs = []
         bits = [None] * k_steps
 
@@ -332,7 +382,8 @@ def main():
         "config": {"workload": "%s batch verify of a %d-round chain, %s" % (
                        sch.name, total, "%d rounds per GPU" % n if weak else "split over %d GPU(s)" % world),
                    "scheme": sch.name, "rounds_total": total, "rounds_per_gpu": n, "global_batch": total,
-                   "parallelism": "round-shard x%d%s" % (world, ", node-wide RLC check (RCCL all-gather)" if node_check else "")},
+                   "parallelism": "round-shard x%d%s" % (world, (", node-wide RLC check (%s all-gather)" % (
+                       "gloo, host-staged" if gloo else "RCCL")) if node_check else "")},
         "roofline": roof,
         "node_roofline_frac": round(value * executed / (peak * world), 4),
         "node_roofline_basis": "executed kernel work %d M/beacon (prep_sig + prep_msg + MSM, bench/workmodel.json "

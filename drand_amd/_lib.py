@@ -16,6 +16,9 @@ DH_EDEVICE = -2
 DH_ENOMEM = -3
 DH_EKEY = -4
 DH_ERECOVER = -5
+DH_EBUSY = -6
+DH_EABANDONED = -7
+DH_NODE_CHECKED = 2
 
 # every symbol declared in include/drandhip.h, with (restype, argtypes)
 _c = ctypes
@@ -46,6 +49,7 @@ SIGNATURES = {
     "dh_hash_to_curve": (_c.c_int, [_c.c_int, _P, _P, _c.c_size_t, _c.c_char_p, _c.c_size_t, _P]),
     "dh_batch_begin": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_size_t, _P, _P, _c.c_size_t, _P, _c.c_size_t, _P,
                                   _c.c_size_t, _P, _P, _c.c_uint64, _P, _c.POINTER(_P), _P]),
+    "dh_batch_check": (_c.c_int, [_P, _P, _c.c_size_t, _P]),
     "dh_check_partials": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_size_t, _P, _c.c_size_t, _c.POINTER(_c.c_int)]),
     "dh_batch_finish": (_c.c_int, [_P, _c.c_int, _P]),
     "dh_profile": (_c.c_int, [_c.c_int]),

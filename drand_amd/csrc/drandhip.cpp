@@ -89,6 +89,9 @@ struct worker {
   // get wave slots ahead of other batches' saturating per-round kernels (verify_core)
   hipStream_t tail = nullptr;
   hipEvent_t handoff = nullptr;
+  // node-wide batch (dh_batch_begin / dh_batch_check): the partial sums are complete (ordered onto the caller's
+  // stream), and the gathered records are complete on the caller's stream (the tail waits for it)
+  hipEvent_t part_ready = nullptr, gath_ready = nullptr;
   bool busy = false;
   // per-round state
   dbuf status, sig_aff, q_pts, scal, entries, verdict_tmp, rand_tmp, h2c_tmp;
@@ -100,6 +103,8 @@ struct worker {
   dbuf in_rounds, in_sigs, in_prevs, in_prev_lens, out_verdict, out_rand;
   // key
   dbuf key_raw, key_aff, key_ok;
+  // node-wide check: the summed (A, B) of the gathered records, and {abandon flag, pairing check, result}
+  dbuf node_sum, node_res;
   // MSM
   dbuf cnt, off, scan_tmp, list, buckets, segs, outA, outB, out2, pass, part, meta;
   // lane-parallel pairing checks
@@ -123,20 +128,31 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den};
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &node_sum, &node_res};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
     if (tail) (void)hipStreamDestroy(tail);
     if (handoff) (void)hipEventDestroy(handoff);
+    if (part_ready) (void)hipEventDestroy(part_ready);
+    if (gath_ready) (void)hipEventDestroy(gath_ready);
     stream = tail = nullptr;
-    handoff = nullptr;
+    handoff = part_ready = gath_ready = nullptr;
   }
 };
 
 struct context {
   std::mutex mu;
+  std::condition_variable freed;  // a worker became idle
   bool inited = false;
   int device = 0;
+  // at most this many workers (2 HIP streams each): a burst of callers waits for an idle worker instead of creating
+  // streams until the runtime runs out of hardware-queue resources (r03: 16 node batches in flight, each holding two
+  // workers, aborted HSA queues with HSA_STATUS_ERROR_OUT_OF_RESOURCES); DRANDHIP_MAX_WORKERS overrides
+  size_t max_workers = [] {
+    const char* e = getenv("DRANDHIP_MAX_WORKERS");
+    const long v = e ? atol(e) : 0;
+    return (size_t)(v >= 1 && v <= 256 ? v : 24);
+  }();
   std::vector<worker*> pool;     // idle or leased workers
   std::vector<worker*> retired;  // leased when dh_shutdown ran: freed by their lease's end
 };
@@ -162,21 +178,33 @@ int ensure_init_locked(uint32_t mask) {
   return DH_OK;
 }
 
+// A worker for the duration of a call. The pool holds at most g_ctx.max_workers: a blocking call waits for an idle
+// one; wait = false (dh_batch_begin, whose lease spans a collective with the other ranks, so waiting could deadlock
+// the node) fails with DH_EBUSY instead.
 struct lease {
   worker* w = nullptr;
   int rc = DH_OK;
-  lease() {
-    std::lock_guard<std::mutex> lk(g_ctx.mu);
+  explicit lease(bool wait = true) {
+    std::unique_lock<std::mutex> lk(g_ctx.mu);
     rc = ensure_init_locked(0);
     if (rc != DH_OK) return;
-    for (worker* x : g_ctx.pool)
-      if (!x->busy) {
-        w = x;
+    for (;;) {
+      for (worker* x : g_ctx.pool)
+        if (!x->busy) {
+          w = x;
+          break;
+        }
+      if (w) break;
+      if (g_ctx.pool.size() < g_ctx.max_workers) {
+        w = new worker();
+        g_ctx.pool.push_back(w);
         break;
       }
-    if (!w) {
-      w = new worker();
-      g_ctx.pool.push_back(w);
+      if (!wait) {
+        rc = fail(DH_EBUSY, "all %zu library workers are busy (DRANDHIP_MAX_WORKERS)", g_ctx.max_workers);
+        return;
+      }
+      g_ctx.freed.wait(lk);
     }
     w->busy = true;
   }
@@ -184,6 +212,7 @@ struct lease {
     if (!w) return;
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     w->busy = false;
+    g_ctx.freed.notify_all();
     auto it = std::find(g_ctx.retired.begin(), g_ctx.retired.end(), w);
     if (it != g_ctx.retired.end()) {  // dh_shutdown ran during this call
       g_ctx.retired.erase(it);
@@ -203,6 +232,32 @@ int set_device_and_stream(worker* w) {
     HIP_TRY(hipStreamCreateWithPriority(&w->tail, hipStreamNonBlocking, greatest));
   }
   if (!w->handoff) HIP_TRY(hipEventCreateWithFlags(&w->handoff, hipEventDisableTiming));
+  if (!w->part_ready) HIP_TRY(hipEventCreateWithFlags(&w->part_ready, hipEventDisableTiming));
+  if (!w->gath_ready) HIP_TRY(hipEventCreateWithFlags(&w->gath_ready, hipEventDisableTiming));
+  return DH_OK;
+}
+
+// The group key decoded on the device (key_aff: the affine point, then [h_eff] pk for G1-signature schemes), cached
+// per worker: a chain's batches all use one key, and decoding a G2 key is a ~9.5 ms one-lane kernel. On a miss the
+// stream is synchronised once to read the key's status; DH_EKEY when it is not a compressed subgroup point.
+int ensure_key(worker* w, bool g2, const uint8_t* pk, size_t pk_len, hipStream_t st) {
+  HIP_TRY(w->key_raw.ensure(96));
+  HIP_TRY(w->key_aff.ensure(96 * 4));  // fixed size keeps the cache valid
+  HIP_TRY(w->key_ok.ensure(64));       // [0] key status, [32..63] RLC seed
+  const bool hit = w->cached_key_len == pk_len && w->cached_key_g2 == (g2 ? 0 : 1) && !memcmp(w->cached_key, pk, pk_len);
+  if (!hit) {
+    w->cached_key_len = 0;
+    uint8_t ok = 0;
+    HIP_TRY(hipMemcpyAsync(w->key_raw.p, pk, pk_len, hipMemcpyHostToDevice, st));
+    HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(), w->key_ok.as<uint8_t>(), st));
+    HIP_TRY(hipMemcpyAsync(&ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    memcpy(w->cached_key, pk, pk_len);
+    w->cached_key_len = pk_len;
+    w->cached_key_g2 = g2 ? 0 : 1;
+    w->cached_key_ok = ok;
+  }
+  if (w->cached_key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
   return DH_OK;
 }
 
@@ -347,12 +402,21 @@ struct prof_entry {
   double ms = 0;
   unsigned long long prods = 0;  // field products executed (counting build only)
 };
+struct prof_pending {
+  const char* name;
+  hipEvent_t a, b;
+  unsigned long long prods;
+};
 struct profiler {
   std::mutex mu;
   std::atomic<bool> on{false};  // read on every launch without the lock
   std::vector<std::pair<std::string, prof_entry>> table;
+  std::vector<prof_pending> pending;  // launches whose end event had not completed when their call returned
   void add(const char* name, float ms, unsigned long long prods = 0) {
     std::lock_guard<std::mutex> lk(mu);
+    add_locked(name, ms, prods);
+  }
+  void add_locked(const char* name, float ms, unsigned long long prods) {
     for (auto& e : table)
       if (e.first == name) {
         e.second.count++;
@@ -368,6 +432,24 @@ struct profiler {
   }
 };
 profiler g_prof;
+
+static void prof_settle(const char* name, hipEvent_t a, hipEvent_t b, unsigned long long prods) {
+  float ms = 0;
+  if (hipEventSynchronize(b) == hipSuccess && hipEventElapsedTime(&ms, a, b) == hipSuccess) g_prof.add(name, ms, prods);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+}
+// resolve the deferred launches (waits for them); called with g_prof.mu held
+static void prof_drain_locked() {
+  for (auto& r : g_prof.pending) {
+    float ms = 0;
+    if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess)
+      g_prof.add_locked(r.name, ms, r.prods);
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  g_prof.pending.clear();
+}
 
 #ifdef DH_COUNT_PRODUCTS
 // counting build: products executed by every translation unit's kernels since the last take
@@ -412,13 +494,16 @@ struct timed_launches {
     recs.push_back(r);
     return e;
   }
+  // launches still running (a node batch's begin returns with its kernels queued) are resolved later, when the
+  // profile is read, so timing never adds a host wait
   void resolve() {
     for (auto& r : recs) {
-      float ms = 0;
-      if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess)
-        g_prof.add(r.name, ms, r.prods);
-      (void)hipEventDestroy(r.a);
-      (void)hipEventDestroy(r.b);
+      if (hipEventQuery(r.b) == hipErrorNotReady) {
+        std::lock_guard<std::mutex> lk(g_prof.mu);
+        g_prof.pending.push_back({r.name, r.a, r.b, r.prods});
+        continue;
+      }
+      prof_settle(r.name, r.a, r.b, r.prods);
     }
     recs.clear();
   }
@@ -603,22 +688,9 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   dh::msm_geom g0{};
   dh::msm_ws ws0{};
   if (mode <= VM_BEGIN) {
-    // key
-    HIP_TRY(w->key_raw.ensure(96));
-    // key-group affine point (G2: 48 words) + [h_eff] pk (48 words, G1 schemes); fixed size keeps the key cache valid
-    HIP_TRY(w->key_aff.ensure(96 * 4));
-    HIP_TRY(w->key_ok.ensure(64));  // [0] key status, [32..63] RLC seed
-    uint8_t key_ok = 0;
-    const bool key_hit = w->cached_key_len == pk_len && w->cached_key_g2 == (g2 ? 0 : 1) && !memcmp(w->cached_key, pk, pk_len);
-    if (key_hit) {
-      key_ok = w->cached_key_ok;
-    } else {
-      w->cached_key_len = 0;
-      HIP_TRY(hipMemcpyAsync(w->key_raw.p, pk, pk_len, hipMemcpyHostToDevice, st));
-      HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(),
-                                    w->key_ok.as<uint8_t>(), st));
-      HIP_TRY(hipMemcpyAsync(&key_ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
-    }
+    // key (cached per worker; a miss synchronises once, before any per-round kernel is queued)
+    int rc = ensure_key(w, g2, pk, pk_len, st);
+    if (rc) return rc;
 
     // per-round prep
     HIP_TRY(w->status.ensure(n));
@@ -627,7 +699,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(w->scal.ensure(n * 16));
     HIP_TRY(w->entries.ensure(n * 4));
     uint32_t seedw[8];
-    int rc = make_seed(seed, seedw);
+    rc = make_seed(seed, seedw);
     if (rc) return rc;
     uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
     // The level-0 sort needs only the scalars, and the scalars only the seed: with a tail stream it runs there
@@ -676,14 +748,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
       HIP_TRY(hipEventRecord(gate->done, st));
       gate->recorded();
     }
-    HIP_TRY(hipStreamSynchronize(st));
-    if (!key_hit) {
-      memcpy(w->cached_key, pk, pk_len);
-      w->cached_key_len = pk_len;
-      w->cached_key_g2 = g2 ? 0 : 1;
-      w->cached_key_ok = key_ok;
-    }
-    if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
+    // no host wait here: the tail below is queued behind the per-round kernels (r03 synchronised the stream at this
+    // point, a host round trip per batch before the MSM could even be queued)
     if (!presorted) HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
   }
   // the tail (MSM, checks, bisection) runs on the worker's high-priority stream, after the per-round kernels
@@ -714,8 +780,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     HIP_TRY(w->outB.ensure(jw * 4));
     HIP_TRY(hipMemsetAsync(w->outA.p, 0, jw * 4, st));
     HIP_TRY(hipMemsetAsync(w->outB.p, 0, jw * 4, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    return DH_OK;
+    return DH_OK;  // queued: dh_batch_begin orders the caller after it (or waits)
   }
   while (m > 0 && gsize > 1) {
     gsize = std::min(gsize, m);
@@ -742,10 +807,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
                               w->outB.as<uint32_t>(), st, w->status.as<uint8_t>(), pre);
       }));
     }
-    if (level == 0 && mode == VM_BEGIN) {
-      HIP_TRY(hipStreamSynchronize(st));
-      return DH_OK;
-    }
+    if (level == 0 && mode == VM_BEGIN) return DH_OK;  // queued; dh_batch_begin orders the caller after it
     if (level == 0 && mode == VM_FINISH_PASS) {  // the node-wide check covers this batch's single level-0 group
       HIP_TRY(hipMemsetAsync(w->pass.p, 1, 1, st));
     } else {
@@ -1268,6 +1330,10 @@ int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t
 }
 
 // ---- node-wide batch check over several processes (one per GPU)
+// A node batch holds ONE worker from dh_batch_begin to dh_batch_finish and runs everything on it: the per-round
+// kernels on its stream, the level-0 MSM, the node-wide check of the gathered records and the bisection on its
+// high-priority tail stream. With a caller stream, nothing in begin / check waits on the host: the partial sums are
+// ordered onto the caller's stream (an event), the collective runs there, and the check is ordered after it.
 struct dh_batch {
   lease* L = nullptr;
   int scheme = 0;
@@ -1282,11 +1348,15 @@ struct dh_batch {
   uint8_t* d_verdict = nullptr;
   uint8_t* d_rand = nullptr;
   hipStream_t st = nullptr;
+  bool checked = false;  // dh_batch_check queued: its result is in the worker's node_res[2]
 };
+
+// one record: A, B (Jacobian AoS) + a status word (0 = this rank's batch began; nonzero = abandoned) + 3 pad words
+static size_t partial_words(bool g2) { return 2 * (g2 ? JAC_WORDS_G2 : JAC_WORDS_G1) + 4; }
 
 int dh_partial_bytes(int scheme) {
   if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
-  return (int)(2 * (sig_on_g2(scheme) ? JAC_WORDS_G2 : JAC_WORDS_G1) * 4);
+  return (int)(partial_words(sig_on_g2(scheme)) * 4);
 }
 
 int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
@@ -1298,20 +1368,18 @@ int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t*
   if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
   if (!pk || !d_partials_out || (n && (!d_rounds || !d_sigs || !d_verdict_out))) return fail(DH_EINVAL, "null argument");
   std::unique_ptr<dh_batch> b(new dh_batch());
-  b->L = new lease();
+  b->L = new lease(false);  // the lease spans the collective: fail (DH_EBUSY) rather than wait for a worker
   if (b->L->rc) {
     int rc = b->L->rc;
     delete b->L;
     return rc;
   }
-  int rc = set_device_and_stream(b->L->w);
+  worker* w = b->L->w;
+  int rc = set_device_and_stream(w);
   if (!rc && hip_stream) {  // inputs produced on the caller's stream
-    hipEvent_t ev;
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, (hipStream_t)hip_stream) != hipSuccess ||
-        hipStreamWaitEvent(b->L->w->stream, ev, 0) != hipSuccess)
+    if (hipEventRecord(w->part_ready, (hipStream_t)hip_stream) != hipSuccess ||
+        hipStreamWaitEvent(w->stream, w->part_ready, 0) != hipSuccess)
       rc = fail(DH_EDEVICE, "cannot order the batch after the caller's stream");
-    else
-      (void)hipEventDestroy(ev);
   }
   b->scheme = scheme;
   b->pk.assign(pk, pk + pk_len);
@@ -1324,21 +1392,31 @@ int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t*
   b->n = n;
   b->d_verdict = d_verdict_out;
   b->d_rand = d_rand_out;
-  b->st = b->L->w->stream;
-  worker* w = b->L->w;
+  b->st = w->stream;
   const size_t jw = sig_on_g2(scheme) ? JAC_WORDS_G2 : JAC_WORDS_G1;
   if (!rc)
     rc = verify_core(w, scheme, pk, pk_len, d_rounds, d_sigs, sig_stride, d_prevs, prev_stride, d_prev_lens, n, d_verdict_out,
                      d_rand_out, seed, b->st, nullptr, nullptr, VM_BEGIN);
-  if (!rc && n) {  // (A, B) of this batch into the caller's device buffer
-    if (hipMemcpyAsync(d_partials_out, w->outA.p, jw * 4, hipMemcpyDeviceToDevice, b->st) != hipSuccess ||
-        hipMemcpyAsync(d_partials_out + jw * 4, w->outB.p, jw * 4, hipMemcpyDeviceToDevice, b->st) != hipSuccess ||
-        hipStreamSynchronize(b->st) != hipSuccess)
-      rc = fail(DH_EDEVICE, "copying the partial sums failed");
-  } else if (!rc) {  // an empty batch contributes the identity (Z = 0)
-    if (hipMemset(d_partials_out, 0, 2 * jw * 4) != hipSuccess) rc = fail(DH_EDEVICE, "hipMemset failed");
+  if (!rc) {
+    // the record (A, B, status 0) on the tail stream, where the level-0 MSM wrote the sums (an empty batch
+    // contributes the identity, Z = 0)
+    hipStream_t ts = w->tail;
+    const bool ok = (n ? hipMemcpyAsync(d_partials_out, w->outA.p, jw * 4, hipMemcpyDeviceToDevice, ts) == hipSuccess &&
+                             hipMemcpyAsync(d_partials_out + jw * 4, w->outB.p, jw * 4, hipMemcpyDeviceToDevice, ts) == hipSuccess
+                       : hipMemsetAsync(d_partials_out, 0, 2 * jw * 4, ts) == hipSuccess) &&
+                    hipMemsetAsync(d_partials_out + 2 * jw * 4, 0, 16, ts) == hipSuccess;
+    if (!ok) {
+      rc = fail(DH_EDEVICE, "writing the partial sums failed");
+    } else if (hip_stream) {  // the caller's stream (the collective) is ordered after the record
+      if (hipEventRecord(w->part_ready, ts) != hipSuccess || hipStreamWaitEvent((hipStream_t)hip_stream, w->part_ready, 0) != hipSuccess)
+        rc = fail(DH_EDEVICE, "cannot order the caller's stream after the partial sums");
+    } else if (hipStreamSynchronize(ts) != hipSuccess) {
+      rc = fail(DH_EDEVICE, "hipStreamSynchronize failed");
+    }
   }
   if (rc) {
+    if (w->stream) (void)hipStreamSynchronize(w->stream);  // nothing queued may outlive the lease
+    if (w->tail) (void)hipStreamSynchronize(w->tail);
     delete b->L;
     return rc;
   }
@@ -1346,66 +1424,93 @@ int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t*
   return DH_OK;
 }
 
+// the node-wide check of k gathered records on worker w's tail stream: sum, one pairing check, res = w->node_res
+static int queue_node_check(worker* w, bool g2, const uint8_t* pk, size_t pk_len, const uint8_t* d_partials, size_t k) {
+  hipStream_t ts = w->tail;
+  int rc = ensure_key(w, g2, pk, pk_len, ts);
+  if (rc) return rc;
+  const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
+  HIP_TRY(w->node_sum.ensure(2 * jw * 4));
+  HIP_TRY(w->node_res.ensure(16));
+  HIP_TRY(hipMemsetAsync(w->node_res.p, 0, 16, ts));
+  uint32_t* sA = w->node_sum.as<uint32_t>();
+  uint8_t* res = w->node_res.as<uint8_t>();
+  HIP_TRY(dh::launch_sum_partials(g2, (const uint32_t*)d_partials, k, partial_words(g2), sA, sA + jw, res, ts));
+  HIP_TRY(group_check(w, g2, sA, sA + jw, 1, w->key_aff.as<uint32_t>(), res + 1, ts, w->key_aff.as<uint32_t>() + 48));
+  return DH_OK;
+}
+
+int dh_batch_check(dh_batch* b, const uint8_t* d_partials, size_t k, void* hip_stream) {
+  if (!b || !d_partials || !k) return fail(DH_EINVAL, "bad node-check arguments");
+  worker* w = b->L->w;
+  const bool g2 = sig_on_g2(b->scheme);
+  if (hip_stream) {  // the gathered records are produced on the caller's stream
+    HIP_TRY(hipEventRecord(w->gath_ready, (hipStream_t)hip_stream));
+    HIP_TRY(hipStreamWaitEvent(w->tail, w->gath_ready, 0));
+  }
+  int rc = queue_node_check(w, g2, b->pk.data(), b->pk.size(), d_partials, k);
+  if (rc) return rc;
+  // passed: every decoded round of this batch is valid, marked on the device
+  HIP_TRY(dh::launch_node_mark(b->n, w->node_res.as<uint8_t>(), w->status.as<uint8_t>(), b->d_verdict, w->tail));
+  b->checked = true;
+  return DH_OK;
+}
+
 int dh_check_partials(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* d_partials, size_t k, int* pass_out) {
   if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
   if (!pk || !d_partials || !pass_out || !k) return fail(DH_EINVAL, "bad node-check arguments");
   const bool g2 = sig_on_g2(scheme);
-  const size_t key_len = g2 ? 48 : 96, jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
+  const size_t key_len = g2 ? 48 : 96;
   if (pk_len != key_len) return fail(DH_EINVAL, "public key must be %zu bytes for scheme %d", key_len, scheme);
   lease L;
   if (L.rc) return L.rc;
   worker* w = L.w;
   int rc = set_device_and_stream(w);
   if (rc) return rc;
-  // the check is a batch's latency-bound tail: on the worker's high-priority stream, like verify_core's, so the other
-  // in-flight batches' per-round kernels do not hold back its one-wave pairing program
-  hipStream_t st = w->tail ? w->tail : w->stream;
-  HIP_TRY(w->key_raw.ensure(96));
-  HIP_TRY(w->key_aff.ensure(96 * 4));  // key + [h_eff] key (k_decode_key)
-  HIP_TRY(w->key_ok.ensure(64));
-  HIP_TRY(w->outA.ensure(jw * 4));
-  HIP_TRY(w->outB.ensure(jw * 4));
-  HIP_TRY(w->pass.ensure(16));
-  // the worker's decoded-key cache, as in verify_core: a chain's batches all check against one key, and decoding a G2
-  // key is a ~9.5 ms one-lane kernel that would sit on every node-wide check (and, had it evicted the cache, on the
-  // next batch of this worker too: the 131k-round per-rank shape ran at 12.5-14.9 M/s against 20.9 locally, r03y)
-  uint8_t key_ok = 0, pass = 0;
-  const bool key_hit = w->cached_key_len == pk_len && w->cached_key_g2 == (g2 ? 0 : 1) && !memcmp(w->cached_key, pk, pk_len);
-  if (key_hit) {
-    key_ok = w->cached_key_ok;
-  } else {
-    w->cached_key_len = 0;
-    HIP_TRY(hipMemcpyAsync(w->key_raw.p, pk, pk_len, hipMemcpyHostToDevice, st));
-    HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(), w->key_ok.as<uint8_t>(), st));
-    HIP_TRY(hipMemcpyAsync(&key_ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
-  }
-  HIP_TRY(dh::launch_sum_partials(g2, (const uint32_t*)d_partials, k, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), st));
-  HIP_TRY(group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), 1, w->key_aff.as<uint32_t>(), w->pass.as<uint8_t>(), st,
-                      w->key_aff.as<uint32_t>() + 48));
-  HIP_TRY(hipMemcpyAsync(&pass, w->pass.p, 1, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  if (!key_hit) {
-    memcpy(w->cached_key, pk, pk_len);
-    w->cached_key_len = pk_len;
-    w->cached_key_g2 = g2 ? 0 : 1;
-    w->cached_key_ok = key_ok;
-  }
-  if (key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
-  *pass_out = pass == 1 ? 1 : 0;
+  rc = queue_node_check(w, g2, pk, pk_len, d_partials, k);
+  if (rc) return rc;
+  uint8_t res[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(res, w->node_res.p, 2, hipMemcpyDeviceToHost, w->tail));
+  HIP_TRY(hipStreamSynchronize(w->tail));
+  *pass_out = 0;
+  if (res[0]) return fail(DH_EABANDONED, "a rank abandoned the node batch (nonzero status word)");
+  *pass_out = res[1] == 1 ? 1 : 0;
   return DH_OK;
 }
 
 int dh_batch_finish(dh_batch* b, int node_pass, uint64_t stats_out[4]) {
   if (!b) return fail(DH_EINVAL, "null batch handle");
-  int rc = DH_OK;
-  if (node_pass >= 0) {
-    rc = verify_core(b->L->w, b->scheme, b->pk.data(), b->pk.size(), b->d_rounds, b->d_sigs, b->sig_stride, b->d_prevs,
+  worker* w = b->L->w;
+  int rc = DH_OK, ret = DH_OK;
+  if (stats_out) memset(stats_out, 0, 4 * sizeof(uint64_t));
+  if (node_pass == DH_NODE_CHECKED) {
+    uint8_t res = 0;
+    if (!b->checked) {
+      rc = fail(DH_EINVAL, "dh_batch_finish(DH_NODE_CHECKED) without dh_batch_check");
+    } else if (hipMemcpyAsync(&res, w->node_res.as<uint8_t>() + 2, 1, hipMemcpyDeviceToHost, w->tail) != hipSuccess ||
+               hipStreamSynchronize(w->tail) != hipSuccess) {
+      rc = fail(DH_EDEVICE, "reading the node-wide check failed");
+    } else if (res == 2) {
+      rc = fail(DH_EABANDONED, "node batch abandoned: dh_batch_begin failed on another rank");
+    } else {
+      ret = res == 1 ? 1 : 0;
+      // passed: the verdicts are already marked (dh_batch_check); the level bookkeeping only when stats are asked
+      if (res != 1 || stats_out)
+        rc = verify_core(w, b->scheme, b->pk.data(), b->pk.size(), b->d_rounds, b->d_sigs, b->sig_stride, b->d_prevs,
+                         b->prev_stride, b->d_prev_lens, b->n, b->d_verdict, b->d_rand, 0, b->st, stats_out, nullptr,
+                         res == 1 ? VM_FINISH_PASS : VM_FINISH);
+    }
+  } else if (node_pass >= 0) {
+    rc = verify_core(w, b->scheme, b->pk.data(), b->pk.size(), b->d_rounds, b->d_sigs, b->sig_stride, b->d_prevs,
                      b->prev_stride, b->d_prev_lens, b->n, b->d_verdict, b->d_rand, 0, b->st, stats_out, nullptr,
                      node_pass ? VM_FINISH_PASS : VM_FINISH);
   }
+  // abandoned or failed: nothing this batch queued may outlive its lease
+  if (w->stream) (void)hipStreamSynchronize(w->stream);
+  if (w->tail) (void)hipStreamSynchronize(w->tail);
   delete b->L;
   delete b;
-  return rc;
+  return rc ? rc : ret;
 }
 
 int dh_verify_beacon(int scheme, const uint8_t* pk, size_t pk_len, uint64_t round, const uint8_t* sig, size_t sig_len,
@@ -1512,7 +1617,7 @@ int dh_recover_batch(int scheme, const uint8_t* commits, int t, int n_nodes, con
                      const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* sig_out,
                      uint8_t* status_out) {
   if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
-  if (t < 1 || n_nodes < 1 || n_nodes > 65535 || !commits || (n_rounds && (!msgs32 || !partials || !part_off ||
+  if (t < 1 || n_nodes < 1 || n_nodes > 65536 || !commits || (n_rounds && (!msgs32 || !partials || !part_off ||
                                                                           !sig_out || !status_out)))
     return fail(DH_EINVAL, "bad Recover arguments");
   for (size_t j = 0; j < n_rounds; j++)
@@ -1528,7 +1633,7 @@ int dh_recover_batch(int scheme, const uint8_t* commits, int t, int n_nodes, con
 int dh_verify_partials_batch(int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
                              const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* ok_out) {
   if (scheme < 0 || scheme > 3) return fail(DH_EINVAL, "unknown scheme %d", scheme);
-  if (t < 1 || n_nodes < 1 || n_nodes > 65535 || !commits || (n_rounds && (!msgs32 || !partials || !part_off || !ok_out)))
+  if (t < 1 || n_nodes < 1 || n_nodes > 65536 || !commits || (n_rounds && (!msgs32 || !partials || !part_off || !ok_out)))
     return fail(DH_EINVAL, "bad VerifyPartial arguments");
   for (size_t j = 0; j < n_rounds; j++)
     if (part_off[j + 1] < part_off[j]) return fail(DH_EINVAL, "part_off must be non-decreasing");
@@ -1663,6 +1768,7 @@ int dh_set_split(uint64_t chunk_rounds, int workers) {
 
 int dh_profile(int enable) {
   std::lock_guard<std::mutex> lk(g_prof.mu);
+  prof_drain_locked();
   g_prof.on = enable != 0;
   g_prof.table.clear();
   return DH_OK;
@@ -1670,6 +1776,7 @@ int dh_profile(int enable) {
 
 int dh_profile_read(char* buf, size_t cap) {
   std::lock_guard<std::mutex> lk(g_prof.mu);
+  prof_drain_locked();
   std::string out = "{";
   bool first = true;
   for (auto& e : g_prof.table) {

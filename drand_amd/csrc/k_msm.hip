@@ -326,21 +326,45 @@ __global__ __launch_bounds__(64) void k_msm_windows(const uint32_t* __restrict__
 }
 
 
-// node-wide check (dh_check_partials): the level-0 sums of k batches, [A_0 | B_0 | A_1 | B_1 ...], added up:
-// thread 0 sums the A points into outA, thread 1 the B points into outB
+// node-wide check (dh_batch_check / dh_check_partials): the records of k batches, each [A | B | status word | pad]
+// (rec_words words), added up: thread 0 sums the A points into outA, thread 1 the B points into outB, thread 2 ORs
+// the ranks' status words into *flag (nonzero: some rank abandoned the batch)
 template <class F>
-__global__ __launch_bounds__(64) void k_sum_partials(const uint32_t* __restrict__ parts, size_t k, uint32_t* __restrict__ outA,
-                                                     uint32_t* __restrict__ outB) {
+__global__ __launch_bounds__(64) void k_sum_partials(const uint32_t* __restrict__ parts, size_t k, size_t rec_words,
+                                                     uint32_t* __restrict__ outA, uint32_t* __restrict__ outB,
+                                                     uint8_t* __restrict__ flag) {
   const int t = threadIdx.x;
+  constexpr size_t JW = 3 * npw<F>::N;  // Jacobian words
+  if (t == 2) {
+    uint32_t any = 0;
+    for (size_t i = 0; i < k; i++) any |= parts[i * rec_words + 2 * JW];
+    if (flag) flag[0] = any ? 1 : 0;
+  }
   if (t > 1) return;
   jac<F> acc = jac_inf<F>();
-  for (size_t i = 0; i < k; i++) acc = jac_add(acc, ld_jac_aos<F>(parts, 2 * i + t));
+  for (size_t i = 0; i < k; i++) acc = jac_add(acc, ld_jac_aos<F>(parts + i * rec_words, t));
   st_jac_aos<F>(t ? outB : outA, 0, acc);
 }
 
-hipError_t launch_sum_partials(int sig_g2, const uint32_t* parts, size_t k, uint32_t* outA, uint32_t* outB, hipStream_t st) {
-  if (sig_g2) hipLaunchKernelGGL(k_sum_partials<fp2>, dim3(1), dim3(64), 0, st, parts, k, outA, outB);
-  else hipLaunchKernelGGL(k_sum_partials<fp>, dim3(1), dim3(64), 0, st, parts, k, outA, outB);
+hipError_t launch_sum_partials(int sig_g2, const uint32_t* parts, size_t k, size_t rec_words, uint32_t* outA, uint32_t* outB,
+                               uint8_t* flag, hipStream_t st) {
+  if (sig_g2) hipLaunchKernelGGL(k_sum_partials<fp2>, dim3(1), dim3(64), 0, st, parts, k, rec_words, outA, outB, flag);
+  else hipLaunchKernelGGL(k_sum_partials<fp>, dim3(1), dim3(64), 0, st, parts, k, rec_words, outA, outB, flag);
+  return hipGetLastError();
+}
+
+// the node-wide verdict of one batch, on the device (no host round trip): res[2] = 2 when some rank abandoned the batch
+// (res[0]), else the pairing check's res[1]; when it passed, every decoded round of the batch is valid
+__global__ void k_node_mark(size_t n, uint8_t* __restrict__ res, const uint8_t* __restrict__ status,
+                            uint8_t* __restrict__ verdict) {
+  const size_t i = gtid();
+  const uint8_t r = res[0] ? 2 : (res[1] == 1 ? 1 : 0);
+  if (i == 0) res[2] = r;
+  if (i < n && r == 1) verdict[i] = status[i] == DEC_OK ? 1 : 0;
+}
+
+hipError_t launch_node_mark(size_t n, uint8_t* res, const uint8_t* status, uint8_t* verdict, hipStream_t st) {
+  hipLaunchKernelGGL(k_node_mark, dim3(nblk(n ? n : 1, 256)), dim3(256), 0, st, n, res, status, verdict);
   return hipGetLastError();
 }
 

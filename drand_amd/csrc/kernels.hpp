@@ -100,8 +100,13 @@ hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngrou
                              uint32_t* out, hipStream_t st);
 hipError_t launch_group_check(int sig_g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_aff,
                               uint8_t* pass, hipStream_t st);
-// node-wide check: sum the k (A, B) level-0 partial-sum pairs laid out [A_0 | B_0 | A_1 | B_1 ...] (Jacobian AoS)
-hipError_t launch_sum_partials(int sig_g2, const uint32_t* parts, size_t k, uint32_t* outA, uint32_t* outB, hipStream_t st);
+// node-wide check: sum the k (A, B) level-0 partial-sum pairs, record i = [A_i | B_i | status word | pad] at
+// parts + i * rec_words (Jacobian AoS); flag[0] (nullable) = 1 when any record's status word is nonzero
+hipError_t launch_sum_partials(int sig_g2, const uint32_t* parts, size_t k, size_t rec_words, uint32_t* outA, uint32_t* outB,
+                               uint8_t* flag, hipStream_t st);
+// res[0] = abandon flag, res[1] = pairing check -> res[2] = 2 abandoned / 1 passed / 0 failed; passed: verdict[i] =
+// (status[i] == DEC_OK) for i < n
+hipError_t launch_node_mark(size_t n, uint8_t* res, const uint8_t* status, uint8_t* verdict, hipStream_t st);
 hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,
                               uint8_t* verdict, hipStream_t st);
 // bisection: out = the entries of the groups with pass == 0, in order; rank[ngroups] = the number of failing groups

@@ -124,22 +124,33 @@ def pack_bits(verdict):
     return (v * w).sum(dim=1).to(torch.uint8)
 
 
-def gather_verdicts(bits, world, group=None):
+class NodeFailure(RuntimeError):
+    """Some rank failed its part of a node-wide step; raised on every rank after the collective."""
+
+
+def gather_verdicts(bits, world, group=None, failed=None):
     """All-gather the ranks' bitmaps (sizes may differ by one byte under strong scaling); returns them in rank
-    order, each trimmed to its own length."""
+    order, each trimmed to its own length. `failed` (a message, or None) marks this rank's part as failed: the flag
+    travels with the sizes, so a rank that failed after the node check still joins the collective and every rank
+    raises NodeFailure instead of waiting for it."""
     import torch
     import torch.distributed as dist
     if world == 1:
+        if failed:
+            raise NodeFailure(failed)
         return [bits]
-    size = torch.tensor([bits.numel()], dtype=torch.int64, device=bits.device)
+    size = torch.tensor([bits.numel(), 1 if failed else 0], dtype=torch.int64, device=bits.device)
     sizes = [torch.zeros_like(size) for _ in range(world)]
     dist.all_gather(sizes, size, group=group)
-    m = int(max(int(x) for x in sizes))
+    bad = [r for r, x in enumerate(sizes) if int(x[1])]
+    if bad:
+        raise NodeFailure(failed or "node step failed on rank(s) %s" % bad)
+    m = int(max(int(x[0]) for x in sizes))
     padded = torch.zeros(m, dtype=bits.dtype, device=bits.device)
     padded[:bits.numel()] = bits
     out = [torch.empty_like(padded) for _ in range(world)]
     dist.all_gather(out, padded, group=group)
-    return [o[:int(k)] for o, k in zip(out, sizes)]
+    return [o[:int(k[0])] for o, k in zip(out, sizes)]
 
 
 def gather_partials(local, world, group=None):
@@ -168,13 +179,44 @@ def rank_seed(seed, rank):
     return int.from_bytes(h.digest()[:8], "little") or 1
 
 
-def verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, partials, world, group=None,
-                      d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=None, rank=None):
-    """One batch of this rank's shard under the node-wide check: dh_batch_begin -> all-gather of the (A, B) sums
-    and a status byte -> dh_check_partials (one pairing check for the whole node) -> dh_batch_finish. `partials` is
-    a uint8 device tensor of dh_partial_bytes(scheme) bytes; the exchange runs on the device under nccl and through
-    host memory otherwise (stage_host=None picks by backend). Returns the node-wide pass flag. If any rank's
-    dh_batch_begin failed, every rank abandons the batch and raises."""
+def _status_offset(pb):
+    """Byte offset of the status word in a partial record of pb bytes: [A | B | status | 3 pad words]."""
+    return pb - 16
+
+
+class NodeBatch:
+    """One batch of this rank's shard under the node-wide check, begun and queued: dh_batch_begin -> all-gather of
+    the partial records -> dh_batch_check, none of which waits on the host under nccl (the collective and the
+    library are ordered through events on torch's current stream). finish() is the batch's one host wait."""
+
+    def __init__(self, lib, b, gathered, err, rank):
+        self.lib, self.b, self.gathered, self.err, self.rank = lib, b, gathered, err, rank
+
+    def finish(self, stats=None):
+        """Wait for the node-wide verdict: True when the node check passed, False when this shard was checked and
+        bisected on its own (verdicts are exact either way). Raises when the batch was abandoned by any rank."""
+        from . import _lib
+        if self.err is not None:
+            raise RuntimeError(self.err)
+        rc = self.lib.dh_batch_finish(self.b, _lib.DH_NODE_CHECKED, stats)
+        self.gathered = None  # the check has read it (finish waited for the batch's streams)
+        if rc == _lib.DH_EABANDONED:
+            raise RuntimeError("node batch abandoned: dh_batch_begin failed on another rank")
+        if rc < 0:
+            raise RuntimeError("rank %d: dh_batch_finish: %s" % (self.rank, _lib.last_error()))
+        return rc == 1
+
+
+def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, partials, world, group=None,
+                     d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=None, rank=None):
+    """Begin one batch under the node-wide check and queue its exchange and check: dh_batch_begin
+    (per-round kernels + level-0 MSM, record written into `partials`, a uint8 device tensor of dh_partial_bytes) ->
+    all-gather of the records -> dh_batch_check (ONE pairing check of the summed records, on this batch's worker).
+    Under nccl the whole chain is queued without a host wait: the library orders torch's current stream (where the
+    collective runs) after the record, and its check after the collective. Under gloo (stage_host) the records go
+    through host memory. A rank whose dh_batch_begin failed still takes part in the exchange with a record whose
+    status word is 1, so every rank's check sees it and abandons the batch (finish raises everywhere) instead of
+    blocking in the collective. Returns a NodeBatch; its finish() waits for the verdicts."""
     import torch
     import torch.distributed as dist
     from . import _lib
@@ -185,55 +227,47 @@ def verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, p
     def ptr(t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
+    stream = torch.cuda.current_stream(partials.device) if partials.is_cuda else None
+    sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
     b = ctypes.c_void_p()
     rc = lib.dh_batch_begin(scheme.id, pk, len(pk), ptr(d_rounds), ptr(d_sigs), scheme.sig_len, ptr(d_prevs),
-                            prev_stride, ptr(d_prev_lens), n, ptr(d_verdict), ptr(d_rand), rank_seed(seed, rank), None,
+                            prev_stride, ptr(d_prev_lens), n, ptr(d_verdict), ptr(d_rand), rank_seed(seed, rank), sp,
                             ctypes.byref(b), ptr(partials))
     err = None if rc == 0 else "rank %d: dh_batch_begin: %s" % (rank, _lib.last_error())
+    pb = partials.numel()
+    if err is not None:  # this rank's record: identity sums, status word 1
+        partials.zero_()
+        partials[_status_offset(pb)] = 1
     if world == 1:
-        if err:
-            raise RuntimeError(err)
-        allp = partials
+        gathered = partials
     else:
-        pb = partials.numel()
         if stage_host is None:
             stage_host = not dist.get_backend(group) == "nccl"
-        dev = torch.device("cpu") if stage_host else partials.device
-        slot = torch.zeros(pb + 4, dtype=torch.uint8, device=dev)
-        if err is None:
-            slot[:pb] = partials.to(dev)  # identity (zeros) otherwise
-        slot[pb] = 0 if err is None else 1
-        gathered = gather_partials(slot, world, group).view(world, pb + 4)
-        status = gathered[:, pb].cpu().numpy()
-        if status.any():
-            if err is None:
-                lib.dh_batch_finish(b, -1, None)
-            bad = [int(r) for r in np.flatnonzero(status)]
-            raise RuntimeError(err or "node batch abandoned: dh_batch_begin failed on rank(s) %s" % bad)
-        allp = gathered[:, :pb].contiguous().to(partials.device)
-    try:
-        if world > 1 and allp.is_cuda:
-            # the gathered sums come from torch's stream and the library reads them from its own: wait for exactly
-            # that work (an event, not a whole-stream or device-wide wait that would also wait for the other
-            # in-flight batches); with one rank the sums are the library's own output, already complete
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(allp.device))
-            ev.synchronize()
-        ok = ctypes.c_int(0)
-        rc = lib.dh_check_partials(scheme.id, pk, len(pk), ptr(allp), world, ctypes.byref(ok))
-        if rc != 0:
-            raise RuntimeError("dh_check_partials: %s" % _lib.last_error())
-    except Exception:
-        lib.dh_batch_finish(b, -1, None)
-        raise
-    rc = lib.dh_batch_finish(b, ok.value, None)
+        slot = partials.cpu() if stage_host else partials
+        gathered = gather_partials(slot, world, group)
+        if stage_host:
+            gathered = gathered.to(partials.device)
+    if err is not None:
+        return NodeBatch(lib, None, None, err, rank)
+    rc = lib.dh_batch_check(b, ptr(gathered), world, sp)
     if rc != 0:
-        raise RuntimeError("dh_batch_finish: %s" % _lib.last_error())
-    return bool(ok.value)
+        e = "rank %d: dh_batch_check: %s" % (rank, _lib.last_error())
+        lib.dh_batch_finish(b, -1, None)
+        return NodeBatch(lib, None, None, e, rank)
+    return NodeBatch(lib, b, gathered, None, rank)
+
+
+def verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, partials, world, group=None,
+                      d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=None, rank=None):
+    """One batch of this rank's shard under the node-wide check, to completion (begin_node_batch + finish). Returns
+    the node-wide pass flag; raises on every rank if any rank's dh_batch_begin failed."""
+    return begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, partials, world, group,
+                            d_prevs=d_prevs, prev_stride=prev_stride, d_prev_lens=d_prev_lens, seed=seed,
+                            stage_host=stage_host, rank=rank).finish()
 
 
 def replay_shard(lib, scheme, pk, first, last, sig_of, rank, world, group=None, prev_of_first=None, seed=0,
-                 device=None):
+                 device=None, stage_host=None):
     """This rank's part of a sharded chain replay (CheckPastBeacons' verification over the node,
     /root/reference/chain/beacon/sync_manager.go:191-225, sharded as SURVEY.md §8e): rounds first..last are split
     with shard_range, and `sig_of` maps each round of this rank's range to its stored signature (a round absent
@@ -269,46 +303,55 @@ def replay_shard(lib, scheme, pk, first, last, sig_of, rank, world, group=None, 
                 continue  # Get fails: previous record missing (trimmed.go:183-187)
             prevs.append(bytes(p))
         idx.append(k)
-    n = len(idx)
-    sigs = np.zeros((max(n, 1), scheme.sig_len), dtype=np.uint8)
-    bad_len = np.zeros(max(n, 1), dtype=bool)
+    # a previous record longer than the device slot (only a corrupted store holds one) stays out of the device batch
+    # (hashing a truncated record would fail the node-wide sums and bisect every rank's whole shard): those rounds
+    # are verified on their own below
+    oversize = [j for j, p in enumerate(prevs) if len(p) > PREV_SLOT_MAX] if scheme.chained else []
+    host_j = set(oversize)
+    dev_j = [j for j in range(len(idx)) if j not in host_j]
+    n = len(dev_j)
+    sigs = np.zeros((max(len(idx), 1), scheme.sig_len), dtype=np.uint8)
+    bad_len = np.zeros(max(len(idx), 1), dtype=bool)
     for j, k in enumerate(idx):
-        s = bytes(sig_of[lo + k])
-        if len(s) == scheme.sig_len:
-            sigs[j] = np.frombuffer(s, np.uint8)
+        s_ = bytes(sig_of[lo + k])
+        if len(s_) == scheme.sig_len:
+            sigs[j] = np.frombuffer(s_, np.uint8)
         else:
             bad_len[j] = True  # an all-zero record never decodes: rejected like kyber's length check
     rounds = np.array([lo + k for k in idx] or [0], dtype=np.uint64)
+    dj = np.array(dev_j, dtype=np.int64)
     d_prevs = d_plen = None
     stride = 0
-    oversize = np.zeros(max(n, 1), dtype=bool)
     if scheme.chained and n:
-        lens = np.array([len(p) for p in prevs], dtype=np.uint32)
-        oversize[:n] = lens > PREV_SLOT_MAX
-        stride = max(96, (int(min(lens.max(), PREV_SLOT_MAX)) + 3) // 4 * 4)
+        lens = np.array([len(prevs[j]) for j in dev_j], dtype=np.uint32)
+        stride = max(96, (int(lens.max()) + 3) // 4 * 4)
         pcol = np.zeros((n, stride), dtype=np.uint8)
-        for j, p in enumerate(prevs):
-            if not oversize[j]:
-                pcol[j, :len(p)] = np.frombuffer(p, np.uint8)
-        lens[oversize[:n]] = 0
+        for t, j in enumerate(dev_j):
+            pcol[t, :len(prevs[j])] = np.frombuffer(prevs[j], np.uint8)
         d_prevs = torch.from_numpy(pcol).to(device)
         d_plen = torch.from_numpy(lens.view(np.int32)).to(device)
-    d_rounds = torch.from_numpy(rounds.view(np.int64)).to(device)
-    d_sigs = torch.from_numpy(sigs).to(device)
+    d_rounds = torch.from_numpy(np.ascontiguousarray(rounds[dj] if n else rounds[:1]).view(np.int64)).to(device)
+    d_sigs = torch.from_numpy(np.ascontiguousarray(sigs[dj] if n else sigs[:1])).to(device)
     d_verdict = torch.zeros(max(n, 1), dtype=torch.uint8, device=device)
     partials = torch.zeros(lib.dh_partial_bytes(scheme.id), dtype=torch.uint8, device=device)
-    verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, None, partials, world, group,
-                      d_prevs=d_prevs, prev_stride=stride, d_prev_lens=d_plen, seed=seed, rank=rank)
-    v = d_verdict.cpu().numpy()[:n].astype(bool) & ~bad_len[:n]
-    if oversize[:n].any():  # previous records beyond the slot: host digest + device pairing check (scheme path)
-        j = np.flatnonzero(oversize[:n])
-        v[j], _ = scheme.verify_beacons(pk, rounds[j], sigs[j], [prevs[i] for i in j], seed=seed,
-                                        want_randomness=False)
-        v[j] &= ~bad_len[j]
+    failed = None
+    v = np.zeros(len(idx), dtype=bool)
+    try:
+        verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, None, partials, world, group,
+                          d_prevs=d_prevs, prev_stride=stride, d_prev_lens=d_plen, seed=seed, rank=rank,
+                          stage_host=stage_host)
+        v[dj] = d_verdict.cpu().numpy()[:n].astype(bool)
+        if oversize:  # host digest + device pairing check (the scheme path routes long records that way)
+            j = np.array(oversize, dtype=np.int64)
+            v[j], _ = scheme.verify_beacons(pk, rounds[j], sigs[j], [prevs[i] for i in j], seed=seed,
+                                            want_randomness=False)
+    except RuntimeError as e:  # joined below, so no rank waits in the verdict gather for this one
+        failed = str(e)
+    v &= ~bad_len[:len(idx)]
     ok_range[np.array(idx, dtype=np.int64)] = v.astype(np.uint8)
     bits = pack_bits(torch.from_numpy(ok_range).to(_collective_device(group) if world > 1 else torch.device("cpu")))
     faulty = []
-    for r_, b_ in enumerate(gather_verdicts(bits, world, group)):
+    for r_, b_ in enumerate(gather_verdicts(bits, world, group, failed=failed)):
         a, z = shard_range(r_, world, last - first + 1)
         got = np.unpackbits(b_.cpu().numpy())[:z - a]
         faulty += [first + a + int(i) for i in np.flatnonzero(got == 0)]

@@ -272,6 +272,51 @@ class Scheme:
 PREV_SLOT_MAX = 4096
 
 
+class ThresholdScheme:
+    """kyber sign.ThresholdScheme over libdrandhip, one call per method — the exact shapes of the cgo type in
+    INTEGRATION.md §2 (gpuThresholdScheme), which the reference's constructors install as Scheme.ThresholdScheme
+    (crypto/schemes.go:101,142,182). Semantics follow kyber v1.1.18 sign/tbls:
+      IndexOf(sig)                          2-byte big-endian prefix (SigShare.Index); error on < 2 bytes
+      VerifyPartial(pubPoly, msg, sig)      Verify(PubPoly.Eval(i).V, msg, sig[2:]) for ANY index i: the call passes
+                                            n_nodes = i + 1 so the device evaluates the polynomial at exactly x = i + 1
+      VerifyRecovered(pk, msg, sig)         bls.Verify (chain/beacon/chainstore.go:207)
+      Recover(pubPoly, msg, sigs, t, n)     first t valid partials in arrival order (wrong-length records skipped, as
+                                            kyber's Verify of sig[2:] rejects them), Lagrange at 0; n_nodes =
+                                            max(n, largest index + 1), so a valid partial of any index counts (kyber)
+    Messages are 32-byte beacon digests on the device; `commits` are the PubPoly's compressed commitments."""
+
+    def __init__(self, scheme):
+        self.scheme = scheme
+
+    def index_of(self, sig):
+        sig = bytes(sig)
+        if len(sig) < 2:
+            raise SchemeError("unexpected EOF")  # binary.Read of the uint16 index
+        return int.from_bytes(sig[:2], "big")
+
+    def verify_partial(self, commits, msg, sig):
+        i = self.index_of(sig)
+        s = self.scheme
+        if len(sig) != 2 + s.sig_len:
+            raise SchemeError("bls: invalid signature")
+        if not s.verify_partials_batch(commits, len(commits), i + 1, [msg], [[sig]])[0][0]:
+            raise SchemeError("bls: invalid signature")
+
+    def verify_recovered(self, pubkey, msg, sig):
+        self.scheme.verify_recovered(pubkey, msg, sig)
+
+    def recover(self, commits, msg, sigs, t, n):
+        s = self.scheme
+        if len(commits) != t:
+            raise SchemeError("the device Recover takes the PubPoly's t commitments")
+        recs = [bytes(x) for x in sigs if len(x) == 2 + s.sig_len]
+        n_nodes = max([n] + [int.from_bytes(x[:2], "big") + 1 for x in recs])
+        out, ok = s.recover_batch(commits, t, n_nodes, [msg], [recs])
+        if not ok[0]:
+            raise SchemeError("share: not enough good public shares to reconstruct secret commitment")
+        return out[0].tobytes()
+
+
 def _pack_prevs(previous_signatures, n):
     """-> (prevs u8[n, stride], lengths u32[n], stride): any lengths up to the stride; the device hashes exactly
     lengths[i] bytes of row i."""

@@ -36,6 +36,8 @@ extern "C" {
 #define DH_ENOMEM (-3)   /* device allocation failed */
 #define DH_EKEY (-4)     /* the group public key does not decode to a subgroup point */
 #define DH_ERECOVER (-5) /* Recover: fewer than t valid partial signatures */
+#define DH_EBUSY (-6)    /* dh_batch_begin: every library worker is held (DRANDHIP_MAX_WORKERS, default 24) */
+#define DH_EABANDONED (-7) /* node-wide batch: some rank's dh_batch_begin failed, every rank abandons the batch */
 
 /* scheme ids, in the order of crypto/schemes.go:206-219 plus the RFC 9380 quicknet scheme */
 #define DH_SCHEME_CHAINED 0      /* "pedersen-bls-chained":   sig G2 (96 B), key G1 (48 B), msg SHA256(prev||round) */
@@ -131,7 +133,8 @@ int dh_randomness_batch(int scheme, const uint8_t* sigs, size_t sig_stride, size
  * of (2 + sig_len) bytes for message msgs32[j] (32-byte digests). Each partial is verified against
  * PubPoly.Eval(index) (commits = t compressed key-group points); the first t valid ones (in the given
  * order) are kept, sorted by index, and Lagrange-interpolated at 0 in the signature group.
- * sig_out: n_rounds * sig_len bytes; status_out[j] = 1 recovered, 0 not enough valid partials.
+ * sig_out: n_rounds * sig_len bytes; status_out[j] = 1 recovered, 0 not enough valid partials. n_nodes <= 65536
+ * (every 2-byte index); a caller that wants kyber's any-index semantics passes max(n, largest index + 1).
  */
 int dh_recover_batch(int scheme, const uint8_t* commits, int t, int n_nodes, const uint8_t* msgs32,
                      const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* sig_out,
@@ -151,21 +154,39 @@ int dh_verify_partials_batch(int scheme, const uint8_t* commits, int t, int n_no
                              const uint8_t* partials, const uint32_t* part_off, size_t n_rounds, uint8_t* ok_out);
 
 /*
- * Node-wide batch check over the GPUs of one node (one process per GPU). Every rank prepares its
- * shard of rounds and its level-0 random-linear-combination sums with dh_batch_begin, which writes
- * dh_partial_bytes(scheme) bytes (A = sum r_i sigma_i, B = sum r_i H(m_i), Jacobian) into d_partials_out (device
- * memory); the ranks all-gather those bytes (RCCL over xGMI); dh_check_partials adds the k gathered pairs and
- * runs ONE pairing check e(g, sum A) = e(pk, [h] sum B) for the whole node; dh_batch_finish then either accepts
- * every decoded round (node_pass = 1) or runs the shard's own level-0 check and bisection (node_pass = 0), so the
- * verdicts are per-round exact either way. node_pass < 0 abandons the batch. The batch keeps one library worker
- * between begin and finish; the arguments of dh_batch_begin must stay valid until dh_batch_finish returns.
+ * Node-wide batch check over the GPUs of one node (one process per GPU; the sharded form of
+ * chain/beacon/sync_manager.go:191-225). Every rank prepares its shard of rounds and its level-0
+ * random-linear-combination sums with dh_batch_begin, which writes one record of dh_partial_bytes(scheme) bytes into
+ * d_partials_out (device memory): A = sum r_i sigma_i, B = sum r_i H(m_i) (Jacobian), a status word (0) and padding.
+ * The ranks all-gather the records (RCCL over xGMI); a rank whose dh_batch_begin failed contributes a record with a
+ * nonzero status word, so every rank learns it from the gathered data. dh_batch_check queues, on the batch's own
+ * worker, the sum of the k gathered records and ONE pairing check e(g, sum A) = e(pk, [h] sum B) for the whole node;
+ * when it passes, every decoded round of the batch is marked valid on the device. dh_batch_finish(b,
+ * DH_NODE_CHECKED, ...) then waits for that result: it returns 1 (the node check passed), or 0 (it failed: the
+ * shard's own level-0 check and bisection ran, so the verdicts are per-round exact either way), or DH_EABANDONED
+ * (some rank's record carried a nonzero status: nothing is valid), or another error.
+ *
+ * Streams: with hip_stream (a hipStream_t, e.g. torch's current stream, on which the collective runs) non-NULL,
+ * dh_batch_begin waits on hip_stream for the inputs, returns as soon as the batch is queued, and makes hip_stream
+ * wait for the record; dh_batch_check makes the check wait for hip_stream's work (the gathered records). Neither
+ * blocks on the host: the only host wait of a batch is in dh_batch_finish. With hip_stream NULL, dh_batch_begin
+ * returns with the record written, and the gathered records must be complete when dh_batch_check is called.
+ *
+ * A batch holds one library worker from begin to finish (DH_EBUSY if none is idle: begin never waits, since the
+ * other ranks may be waiting in the collective); the arguments of dh_batch_begin must stay valid until
+ * dh_batch_finish returns. dh_batch_finish with node_pass 1 / 0 (a result the caller obtained itself, e.g. from
+ * dh_check_partials) accepts every decoded round / runs the shard's own check and returns DH_OK; node_pass < 0
+ * (other than DH_NODE_CHECKED) abandons the batch. dh_check_partials is the standalone check of k records (it
+ * leases its own worker and blocks): pass_out = 1 / 0, DH_EABANDONED when a status word is nonzero.
  */
 typedef struct dh_batch dh_batch;
+#define DH_NODE_CHECKED 2 /* dh_batch_finish: take the result of dh_batch_check */
 int dh_partial_bytes(int scheme);
 int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                    size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
                    uint8_t* d_verdict_out, uint8_t* d_rand_out, uint64_t seed, void* hip_stream, dh_batch** batch_out,
                    uint8_t* d_partials_out);
+int dh_batch_check(dh_batch* batch, const uint8_t* d_partials, size_t k, void* hip_stream);
 int dh_check_partials(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* d_partials, size_t k, int* pass_out);
 int dh_batch_finish(dh_batch* batch, int node_pass, uint64_t stats_out[4]);
 

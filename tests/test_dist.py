@@ -123,31 +123,32 @@ def test_pack_bits_matches_numpy():
 
 
 class _FakeLib:
-    """The three node-check entry points of libdrandhip, on the host: dh_batch_begin writes rank-specific partial
-    bytes (or fails on `fail_rank`), dh_check_partials records what the all-gather delivered."""
+    """The node-check entry points of libdrandhip, on the host: dh_batch_begin writes a rank-specific record (or
+    fails on `fail_rank`), dh_batch_check records what the all-gather delivered and whether a status word was set,
+    dh_batch_finish(DH_NODE_CHECKED) reports it like the library (1 passed, DH_EABANDONED)."""
 
     def __init__(self, rank, fail_rank, pb):
         self.rank, self.fail_rank, self.pb = rank, fail_rank, pb
-        self.seed, self.seen, self.finished = None, None, []
+        self.seed, self.seen, self.finished, self.abandoned = None, None, [], False
 
     def dh_batch_begin(self, sid, pk, pklen, r, s, sl, p, ps, pl, n, v, rnd, seed, stream, bref, parts):
         import ctypes
         self.seed = seed
         if self.rank == self.fail_rank:
             return -2
-        ctypes.memmove(parts.value, bytes([self.rank + 1]) * self.pb, self.pb)
+        ctypes.memmove(parts.value, bytes([self.rank + 1]) * (self.pb - 16) + bytes(16), self.pb)
         bref._obj.value = 1000 + self.rank
         return 0
 
-    def dh_check_partials(self, sid, pk, pklen, allp, k, okref):
+    def dh_batch_check(self, b, allp, k, stream):
         import ctypes
         self.seen = ctypes.string_at(allp.value, k * self.pb)
-        okref._obj.value = 1
+        self.abandoned = any(self.seen[i * self.pb + self.pb - 16] for i in range(k))
         return 0
 
-    def dh_batch_finish(self, b, ok, st):
-        self.finished.append(ok)
-        return 0
+    def dh_batch_finish(self, b, mode, st):
+        self.finished.append(mode)
+        return -7 if self.abandoned else 1
 
 
 def _node_worker(rank, world, port, fail_rank, q):
@@ -156,7 +157,7 @@ def _node_worker(rank, world, port, fail_rank, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from drand_amd.scheme import scheme_from_name
     s = scheme_from_name("pedersen-bls-unchained")
-    pb = 2 * 72 * 4
+    pb = 2 * 72 * 4 + 16
     lib = _FakeLib(rank, fail_rank, pb)
     parts = torch.zeros(pb, dtype=torch.uint8)
     out = {"rank": rank}
@@ -164,6 +165,12 @@ def _node_worker(rank, world, port, fail_rank, q):
         out["pass"] = verify_node_batch(lib, s, b"k" * 48, None, None, 10, None, None, parts, world, seed=5)
     except RuntimeError as e:
         out["error"] = str(e)
+    # a rank that failed after the node check still joins the verdict gather, and every rank raises
+    try:
+        gather_verdicts(torch.zeros(2, dtype=torch.uint8), world, failed="boom" if rank == 2 else None)
+        out["gather"] = "ok"
+    except RuntimeError as e:
+        out["gather"] = str(e)
     out.update(seed=lib.seed, seen=lib.seen, finished=lib.finished)
     q.put(out)
     dist.barrier()
@@ -173,9 +180,10 @@ def _node_worker(rank, world, port, fail_rank, q):
 @pytest.mark.parametrize("fail_rank", [None, 1])
 def test_node_batch_protocol_gloo(fail_rank):
     """verify_node_batch's collective protocol at world 3 over gloo (library entry points faked on the host): the
-    partial sums arrive in rank order at every rank, each rank's RLC seed is distinct (rank_seed), and when
-    dh_batch_begin fails on one rank every rank raises instead of blocking in the all-gather, the ranks that began
-    abandoning their batch (dh_batch_finish(b, -1))."""
+    partial records arrive in rank order at every rank, each rank's RLC seed is distinct (rank_seed); when
+    dh_batch_begin fails on one rank, its record carries status 1, every other rank's check sees it and its finish
+    reports the batch abandoned, so every rank raises instead of blocking in the all-gather; and a failure flagged
+    in the verdict gather raises on every rank."""
     world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -188,12 +196,16 @@ def test_node_batch_protocol_gloo(fail_rank):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert len({m["seed"] for m in res}) == world and res[0]["seed"] == rank_seed(5, 0) != 5
-    pb = 2 * 72 * 4
+    pb = 2 * 72 * 4 + 16
+    recs = [bytes([r + 1]) * (pb - 16) + bytes(16) for r in range(world)]
     if fail_rank is None:
-        assert all(m["pass"] is True and m["finished"] == [1] for m in res)
-        assert all(m["seen"] == b"".join(bytes([r + 1]) * pb for r in range(world)) for m in res)
+        assert all(m["pass"] is True and m["finished"] == [2] for m in res)
+        assert all(m["seen"] == b"".join(recs) for m in res)
     else:
-        assert all("error" in m and m["seen"] is None for m in res)
-        assert "dh_batch_begin" in res[fail_rank]["error"] and "rank(s) [1]" in res[0]["error"]
-        assert [m["finished"] for m in res] == [[-1], [], [-1]]
+        assert all("error" in m for m in res)
+        assert "dh_batch_begin" in res[fail_rank]["error"] and "abandoned" in res[0]["error"]
+        assert [m["finished"] for m in res] == [[2], [], [2]]
+        recs[fail_rank] = bytes(pb - 16) + bytes([1]) + bytes(15)
+        assert res[0]["seen"] == b"".join(recs) and res[fail_rank]["seen"] is None
+    assert res[2]["gather"] == "boom" and all("rank(s) [2]" in m["gather"] for m in res[:2])
     assert rank_seed(0, 3) == 0

@@ -86,13 +86,17 @@ def _oracle_replay(oracle, name, pk, sig_of, first, last):
 
 
 # ---------------------------------------------------------------- node-wide check, in one process
+@pytest.mark.parametrize("mode", ["device", "host"])
 @pytest.mark.parametrize("name", ["bls-unchained-g1-rfc9380", "pedersen-bls-unchained", CHAINED, "bls-unchained-on-g1"])
-def test_node_wide_check_all_schemes(dh, oracle, name):
+def test_node_wide_check_all_schemes(dh, oracle, name, mode):
     """Three shards begun as three batches — one of them a single round, which contributes the identity — their
-    level-0 sums combined by dh_check_partials (ONE pairing check), then finished. A clean chain passes the node
-    check and every round is accepted; with a corruption on the shard boundary (chained: the last round of shard 0
-    stores another round's signature, so round k and k+1 fail, k+1 being the one-round shard) the node check fails
-    and each shard's own check + bisection gives the oracle's verdicts."""
+    level-0 sums combined by ONE pairing check, then finished. mode "device": the protocol the multi-GPU bench and
+    replay run — dh_batch_begin ordered onto torch's stream, then per batch dh_batch_check of the three records on its
+    own worker (no host wait) and dh_batch_finish(DH_NODE_CHECKED), which returns 1 / 0; mode "host": the standalone
+    dh_check_partials and an explicit node_pass. A clean chain passes the node check and every round is accepted; with
+    a corruption on the shard boundary (chained: the last round of shard 0 stores another round's signature, so round k
+    and k+1 fail, k+1 being the one-round shard) the node check fails and each shard's own check + bisection gives the
+    oracle's verdicts."""
     import torch
     from drand_amd import _lib
     lib = _lib.load()
@@ -109,7 +113,7 @@ def test_node_wide_check_all_schemes(dh, oracle, name):
     rounds = np.arange(1, n + 1, dtype=np.uint64)
     dev = torch.device("cuda", 0)
     pb = lib.dh_partial_bytes(s.id)
-    assert pb == 2 * (72 if s.sig_len == 96 else 36) * 4
+    assert pb == 2 * (72 if s.sig_len == 96 else 36) * 4 + 16
 
     def run(sig_arr, seed):
         prev = np.zeros((n, 96), np.uint8)
@@ -126,6 +130,8 @@ def test_node_wide_check_all_schemes(dh, oracle, name):
         parts = torch.zeros(len(shards) * pb, dtype=torch.uint8, device=dev)
         handles = []
         sl = s.sig_len
+        cur = torch.cuda.current_stream(dev)
+        sp = ctypes.c_void_p(cur.cuda_stream) if mode == "device" else None
         for k, (lo, hi) in enumerate(shards):
             b = ctypes.c_void_p()
             rc = lib.dh_batch_begin(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr() + 8 * lo),
@@ -133,10 +139,26 @@ def test_node_wide_check_all_schemes(dh, oracle, name):
                                     ctypes.c_void_p(d_p.data_ptr() + 96 * lo) if s.chained else None,
                                     96 if s.chained else 0,
                                     ctypes.c_void_p(d_l.data_ptr() + 4 * lo) if s.chained else None, hi - lo,
-                                    ctypes.c_void_p(d_v.data_ptr() + lo), None, seed + 101 * k, None, ctypes.byref(b),
+                                    ctypes.c_void_p(d_v.data_ptr() + lo), None, seed + 101 * k, sp, ctypes.byref(b),
                                     ctypes.c_void_p(parts.data_ptr() + k * pb))
             assert rc == 0, _lib.last_error()
             handles.append(b)
+        if mode == "device":
+            # the records are complete in the current stream's order: a copy queued there sees them
+            snap = parts.clone()
+            results, stats = [], []
+            for b in handles:
+                assert lib.dh_batch_check(b, ctypes.c_void_p(parts.data_ptr()), len(shards), sp) == 0, _lib.last_error()
+            for b in handles:
+                st = (ctypes.c_uint64 * 4)()
+                r = lib.dh_batch_finish(b, _lib.DH_NODE_CHECKED, st)
+                assert r in (0, 1), _lib.last_error()
+                results.append(r)
+                stats.append(list(st))
+            torch.cuda.synchronize()
+            assert not snap[pb:2 * pb].cpu().numpy().any(), "a one-round shard must contribute the identity"
+            assert len(set(results)) == 1  # every batch saw the same node-wide result
+            return results[0], d_v.cpu().numpy().astype(bool), stats
         torch.cuda.synchronize()
         one = parts[pb:2 * pb].cpu().numpy()
         assert not one.any(), "a one-round shard must contribute the identity"
@@ -173,6 +195,42 @@ def test_node_wide_check_all_schemes(dh, oracle, name):
     assert np.array_equal(ref, v)
 
 
+def test_node_batch_abandoned(dh):
+    """A gathered record whose status word is nonzero (a rank whose dh_batch_begin failed) makes the node-wide check
+    abandon the batch: dh_batch_finish(DH_NODE_CHECKED) returns DH_EABANDONED and marks no round valid, and
+    dh_check_partials returns DH_EABANDONED too."""
+    import torch
+    from drand_amd import _lib
+    lib = _lib.load()
+    s = dh.scheme_from_name("bls-unchained-g1-rfc9380")
+    sk = _secret(b"abandon")
+    pk = s.public_key(sk)
+    n = 2048
+    rounds = np.arange(1, n + 1, dtype=np.uint64)
+    dev = torch.device("cuda", 0)
+    d_r = torch.from_numpy(rounds.view(np.int64)).to(dev)
+    d_s = torch.from_numpy(s.sign_beacons(sk, rounds)).to(dev)
+    d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+    pb = lib.dh_partial_bytes(s.id)
+    parts = torch.zeros(2 * pb, dtype=torch.uint8, device=dev)
+    parts[2 * pb - 16] = 1  # the second rank's record: began nothing, status 1
+    sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    b = ctypes.c_void_p()
+    assert lib.dh_batch_begin(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr()), ctypes.c_void_p(d_s.data_ptr()), 48,
+                              None, 0, None, n, ctypes.c_void_p(d_v.data_ptr()), None, 3, sp, ctypes.byref(b),
+                              ctypes.c_void_p(parts.data_ptr())) == 0, _lib.last_error()
+    assert lib.dh_batch_check(b, ctypes.c_void_p(parts.data_ptr()), 2, sp) == 0, _lib.last_error()
+    assert lib.dh_batch_finish(b, _lib.DH_NODE_CHECKED, None) == _lib.DH_EABANDONED
+    torch.cuda.synchronize()
+    assert not d_v.cpu().numpy().any()
+    ok = ctypes.c_int(-1)
+    assert lib.dh_check_partials(s.id, pk, len(pk), ctypes.c_void_p(parts.data_ptr()), 2, ctypes.byref(ok)) == \
+        _lib.DH_EABANDONED
+    parts[2 * pb - 16] = 0  # the same records with status 0: the node check passes (identity + the batch's sums)
+    assert lib.dh_check_partials(s.id, pk, len(pk), ctypes.c_void_p(parts.data_ptr()), 2, ctypes.byref(ok)) == 0
+    assert ok.value == 1
+
+
 # ---------------------------------------------------------------- two processes, gloo, one GPU
 def _free_port():
     so = socket.socket()
@@ -182,7 +240,7 @@ def _free_port():
     return p
 
 
-def _replay_worker(rank, world, port, name, pk, first, last, local, genesis, q):
+def _replay_worker(rank, world, port, name, pk, first, last, local, genesis, q, stage_host=None):
     try:
         import torch
         import torch.distributed as dist
@@ -198,7 +256,8 @@ def _replay_worker(rank, world, port, name, pk, first, last, local, genesis, q):
         s = scheme_from_name(name)
         res = []
         for case_local in local:
-            res.append(replay_shard(lib, s, pk, first, last, case_local, rank, world, prev_of_first=genesis, seed=0))
+            res.append(replay_shard(lib, s, pk, first, last, case_local, rank, world, prev_of_first=genesis, seed=0,
+                                    stage_host=stage_host))
         q.put({"rank": rank, "faulty": res})
         dist.barrier()
         dist.destroy_process_group()
@@ -207,12 +266,15 @@ def _replay_worker(rank, world, port, name, pk, first, last, local, genesis, q):
         q.put({"rank": rank, "error": repr(e) + traceback.format_exc()})
 
 
-def test_replay_shard_two_processes(dh, oracle):
+@pytest.mark.parametrize("stage_host", [None, False])
+def test_replay_shard_two_processes(dh, oracle, stage_host):
     """dist.replay_shard in two spawned processes (gloo, both on GPU 0): a sequential chained chain of 3000 rounds,
     (a) round hi0 (the last round of rank 0) stores round hi0-1's signature: hi0 fails and so does hi0+1, the
     first round of rank 1, whose previous signature reaches it only through exchange_halo; (b) round hi0 is missing:
     hi0 and hi0+1 are reported missing (Get error) through MISSING_HALO; (c) the clean chain. Each whole-node faulty
-    set equals the serial oracle replay over the unsharded store."""
+    set equals the serial oracle replay over the unsharded store. stage_host=False keeps the records on the device
+    (gloo's CUDA all-gather): the device-ordered branch of begin_node_batch — the library orders torch's stream after
+    the record and its check after the collective — which the nccl backend takes on a multi-GPU node."""
     import torch.multiprocessing as mp
     from drand_amd.dist import shard_range
     s = dh.scheme_from_name(CHAINED)
@@ -233,7 +295,8 @@ def test_replay_shard_two_processes(dh, oracle):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_replay_worker, args=(r, world, port, CHAINED, pk, 1, n, local[r], GENESIS, q))
+    procs = [ctx.Process(target=_replay_worker, args=(r, world, port, CHAINED, pk, 1, n, local[r], GENESIS, q,
+                                                      stage_host))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -279,3 +342,27 @@ def test_relay_s3_sync_device(dh, oracle):
         for r in up:
             body = json.loads(bucket["public/%d" % r])
             assert base64.b64decode(body["randomness"]) == hashlib.sha256(recs[r]["signature"]).digest()
+
+
+# ---------------------------------------------------------------- bench.py --gpus N launches N ranks
+def test_bench_launches_ranks():
+    """`python bench.py --gpus 2` with no launcher spawns the two ranks itself (torch.distributed.run in a child
+    process, before any HIP call) and prints rank 0's line: n_gpus 2, the node-wide check as the parallelism, every
+    verdict valid. gloo rehearsal: both ranks on GPU 0, strong scaling of a 262,144-round chain."""
+    import subprocess
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--total-rounds", "262144",
+           "--steps", "2", "--warmup", "1", "--streams", "4", "--no-cpu-baseline", "--roofline-steps", "0",
+           "--single-call-steps", "0"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, out.stdout[-2000:]
+    res = json.loads(line[0])
+    assert res["n_gpus"] == 2 and res["verdicts_ok"] is True and res["scaling"] == "strong"
+    assert "node-wide RLC check" in res["config"]["parallelism"] and res["config"]["rounds_per_gpu"] == 131072
+    # under a launcher WORLD_SIZE must match --gpus
+    bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True, text=True,
+                         env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), timeout=120)
+    assert bad.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in bad.stderr

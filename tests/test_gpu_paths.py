@@ -399,7 +399,7 @@ def test_node_wide_check_protocol(dh):
     pk = s.public_key(sk)
     dev = torch.device("cuda", 0)
     pb = lib.dh_partial_bytes(s.id)
-    assert pb == 2 * 36 * 4
+    assert pb == 2 * 36 * 4 + 16  # A, B, status word, padding
 
     def run(sig_arr):
         half = [(0, 5000), (5000, n)]
@@ -522,3 +522,87 @@ def test_group_checks_pass_on_clean_batches(dh, scheme):
     # bisection levels on G1 and G2)
     assert st2[1] == st2[0], st2
     assert 1 <= st2[2] <= (n if st2[0] == 1 else 1024), st2
+
+
+# ---------------------------------------------------------------- the MSM's exact path for exceptional additions
+@pytest.mark.parametrize("scheme", ["bls-unchained-g1-rfc9380", "pedersen-bls-unchained"])
+def test_msm_exceptional_cases(dh, scheme):
+    """Thousands of copies of ONE valid beacon: every bucket of every window receives the same signature point (and
+    the same hash point) with both signs, so the bucket pass meets P + P and P - P, and the bucket sums, being small
+    multiples of one point, collide again in the segment sums, the tree and the window Horner. Each such addition
+    leaves Z = 0 in the fast formulas and must be recomputed on the exact path (k_msm.hip MSM28). The batch must still
+    pass its single level-0 check — stats [1 level, 0 failed groups, 0 leaf rounds] — since a broken exact path would
+    fail the check and show up only as bisection levels (the verdicts would still be right)."""
+    import ctypes
+    import torch
+    from drand_amd import _lib
+    lib = _lib.load()
+    s = dh.scheme_from_name(scheme)
+    sk = _secret(b"exceptional-" + scheme.encode())
+    pk = s.public_key(sk)
+    n = 20000 if s.sig_len == 48 else 8000
+    rounds = np.full(n, 123457, dtype=np.uint64)
+    sigs = np.ascontiguousarray(np.repeat(s.sign_beacons(sk, rounds[:1]), n, axis=0))
+    dev = torch.device("cuda", 0)
+    d_r = torch.from_numpy(rounds.view(np.int64)).to(dev)
+    d_s = torch.from_numpy(sigs).to(dev)
+    for seed in (3, 4):
+        d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+        st = (ctypes.c_uint64 * 4)()
+        rc = lib.dh_verify_batch_device(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr()), ctypes.c_void_p(d_s.data_ptr()),
+                                        s.sig_len, None, 0, None, n, ctypes.c_void_p(d_v.data_ptr()), None, seed, None, st)
+        assert rc == 0, _lib.last_error()
+        torch.cuda.synchronize()
+        assert d_v.cpu().numpy().all()
+        assert list(st) == [1, 0, 0, 0], list(st)
+
+
+# ---------------------------------------------------------------- the Go sign.ThresholdScheme drop-in, call by call
+@pytest.mark.parametrize("scheme", ["pedersen-bls-unchained", "bls-unchained-g1-rfc9380"])
+def test_threshold_scheme_dropin_shapes(dh, oracle, scheme):
+    """drand_amd.scheme.ThresholdScheme makes exactly the C calls of the cgo gpuThresholdScheme
+    — dh_verify_recovered with one digest, dh_verify_partials_batch with one partial and n_nodes = index + 1,
+    dh_recover_batch with one round and n_nodes = max(n, largest index + 1) — and each result equals kyber sign/tbls
+    restated by the oracle: any index is evaluated (a valid partial of index 11 in a group of n = 8 verifies and counts
+    toward Recover, as in kyber), wrong-length records are never kept, fewer than t valid partials is an error."""
+    from drand_amd.scheme import SchemeError, ThresholdScheme
+    s = dh.scheme_from_name(scheme)
+    ts = ThresholdScheme(s)
+    n, t = 8, 5
+    coeffs, commits = _dealer(s, t, b"dropin-" + scheme.encode())
+    pk = commits[0]
+    rounds = np.array([424242, 424243], dtype=np.uint64)
+    msgs = [s.digest_beacon(int(r)) for r in rounds]
+    idx = list(range(n)) + [11]
+    share_sigs = {i: s.sign_beacons(_share(coeffs, i), rounds) for i in idx}
+    part = {i: i.to_bytes(2, "big") + share_sigs[i][0].tobytes() for i in idx}
+    other = 3 .to_bytes(2, "big") + share_sigs[3][1].tobytes()  # index 3, the other round's signature
+    # IndexOf
+    assert ts.index_of(part[11]) == 11 and ts.index_of(b"\x01\x02") == 258
+    with pytest.raises(SchemeError):
+        ts.index_of(b"\x01")
+    # VerifyRecovered: the group signature [f(0)] H(m)
+    group = s.sign_beacons(coeffs[0].to_bytes(32, "big"), rounds)[0].tobytes()
+    assert oracle.verify(s.name, pk, msgs[0], group)
+    ts.verify_recovered(pk, msgs[0], group)
+    bad = bytearray(group)
+    bad[-1] ^= 1
+    with pytest.raises(SchemeError):
+        ts.verify_recovered(pk, msgs[0], bytes(bad))
+    with pytest.raises(SchemeError):
+        ts.verify_recovered(pk, msgs[1], group)
+    # VerifyPartial, any index (kyber evaluates PubPoly.Eval(i) for every i)
+    for i in (0, 5, 7, 11):
+        assert oracle.verify(s.name, oracle.pubpoly_eval(s.name, commits, i), msgs[0], part[i][2:])
+        ts.verify_partial(commits, msgs[0], part[i])
+    for p in (other, part[4][:-1], part[2][:2] + part[6][2:]):  # wrong round, short record, another share's sig
+        with pytest.raises(SchemeError):
+            ts.verify_partial(commits, msgs[0], p)
+    # Recover: arrival order with an invalid partial, a wrong-length record and the index-11 share among the first t
+    arrivals = [other, part[11], part[0][:-3], part[6], part[2], part[9 % n], part[4], part[7], part[3]]
+    got = ts.recover(commits, msgs[0], arrivals, t, n)
+    want = oracle.recover(s.name, commits, t, n, msgs[0], [p for p in arrivals if len(p) == 2 + s.sig_len])
+    assert want is not None and got == want == group
+    with pytest.raises(SchemeError, match="not enough good public shares"):
+        ts.recover(commits, msgs[0], [other, part[1], part[2], part[11], part[5][:-1]], t, n)
+    assert oracle.recover(s.name, commits, t, n, msgs[0], [other, part[1], part[2], part[11]]) is None
