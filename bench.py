@@ -199,6 +199,7 @@ def main():
     d_rand = [torch.zeros((n, 32), dtype=torch.uint8, device=dev) for _ in range(S)]
     pbytes = lib.dh_partial_bytes(sch.id)
     d_part = [torch.zeros(pbytes, dtype=torch.uint8, device=dev) for _ in range(S)]
+    slot_streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
     torch.cuda.synchronize()
     state = {"node_check": node_check}
 
@@ -219,17 +220,24 @@ def main():
 
         def retire():
             slot, h = pending.popleft()
-            h.finish()
-            bits.append(pack_bits(d_verdict[slot]))
+            with torch.cuda.stream(slot_streams[slot]):
+                h.finish()
+                bits.append(pack_bits(d_verdict[slot]))
 
         for k in range(k_steps):
             if len(pending) == streams:
                 retire()
             slot = k % streams
-            pending.append((slot, begin_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot], d_rand[slot],
-                                                   d_part[slot], world, None, stage_host=gloo, rank=rank)))
+            # each slot's begin / collective / check are ordered on the slot's own torch stream: an input-ordering
+            # event on one shared stream would also carry that stream's wait for the previous batch's record, and
+            # chain every batch's per-round kernels behind the previous batch's MSM (r04a: 14.2 M/s at 131k, 8 slots)
+            with torch.cuda.stream(slot_streams[slot]):
+                pending.append((slot, begin_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot],
+                                                       d_rand[slot], d_part[slot], world, None, stage_host=gloo,
+                                                       rank=rank)))
         while pending:
             retire()
+        torch.cuda.synchronize()
         if world > 1 and gather and k_steps:
             b = torch.cat(bits)
             gather_verdicts(b.cpu() if gloo else b, world)

@@ -99,6 +99,8 @@ struct worker {
   dbuf s28, q28;
   // bisection on the device: the next level's entries, fail flags, their ranks and the scan's block sums
   dbuf entries_alt, cflags, crank, cscan;
+  // bisection from scaled points: [r_i] sigma_i and [r_i] H_i (launch_scale28), the level sums' temporaries
+  dbuf tree_r, tree_a, tree_b;
   // host-API staging
   dbuf in_rounds, in_sigs, in_prevs, in_prev_lens, out_verdict, out_rand;
   // key
@@ -128,7 +130,8 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &node_sum, &node_res};
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &node_sum, &node_res, &tree_r,
+                   &tree_a, &tree_b};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
     if (tail) (void)hipStreamDestroy(tail);
@@ -577,21 +580,23 @@ static const std::vector<size_t>& fixed_ladder() {
 // latency floor), per-round leaf checks ~12 + 0.005 m. Faults are modelled as Poisson at the density the last
 // level observed (faulty groups -> -ln(1 - f) faults per group, at least one per failing group; when every
 // group failed, 5 per group). The next size minimises the expected cost of the rest of the descent.
-static double msm_cost_ms(double m, size_t g) {
+static double msm_cost_ms(double m, size_t g, bool tree) {
+  // from scaled points a level's sums are ~1 point addition per entry (launch_group_sums28)
+  if (tree) return 0.5 + 1e-6 * m;
   const dh::msm_geom gg = geom_for(g, 2);
   return 9.0 + 1.8e-6 * m * (double)(gg.nwin * gg.halves) / 2.0;  // fitted on 127-bit entries (8 per round at c = 16)
 }
 static double check_cost_ms(double groups) { return 12.0 + 0.0025 * groups; }
 static double leaf_cost_ms(double m) { return 12.0 + 0.005 * m; }
 
-static double descent_cost(double m, double d, size_t gprev, size_t* best) {
+static double descent_cost(double m, double d, size_t gprev, size_t* best, bool tree) {
   double c_best = leaf_cost_ms(m);
   if (best) *best = 1;
   for (size_t g = 4; g < gprev && (double)g < m; g *= 4) {
     const double q = -std::expm1(-d * (double)g);  // P(group of g holds a fault)
     const double m_next = m * q;
-    const double c = msm_cost_ms(m, g) + check_cost_ms(m / (double)g) +
-                     (m_next < 1.0 ? 0.0 : descent_cost(m_next, d / std::max(q, 1e-12), g, nullptr));
+    const double c = msm_cost_ms(m, g, tree) + check_cost_ms(m / (double)g) +
+                     (m_next < 1.0 ? 0.0 : descent_cost(m_next, d / std::max(q, 1e-12), g, nullptr, tree));
     if (c < c_best) {
       c_best = c;
       if (best) *best = g;
@@ -600,25 +605,36 @@ static double descent_cost(double m, double d, size_t gprev, size_t* best) {
   return c_best;
 }
 
-static size_t next_group_size(size_t gsize, size_t ngroups, size_t nfail, size_t m_prev, size_t m_next, double hint) {
+static size_t next_group_size(size_t gsize, size_t ngroups, size_t nfail, size_t m_prev, size_t m_next, double hint,
+                              bool tree) {
   // level 0 (one group) says only that some round is bad: 1024 costs about what 4096 does over 1M rounds and
   // its groups still pass at a 0.1% fault density (4096-round groups then all fail). When the worker's previous
   // bisection saw dense faults (> 1 per 2000 rounds: most 1024-groups fail), 256-round groups first: the ladder
   // sweep on a 0.2%-faulty chained window put 256-first ladders 5-9% ahead of 1024-first ones
   // (profiles/bisect_sweep_r03s.txt)
   const bool dense = hint > 1.0 / 2000;
-  if (gsize == m_prev && m_prev > 4096) return dense ? 256 : 1024;
+  if (gsize == m_prev && m_prev > 4096 && !tree) return dense ? 256 : 1024;
   // ... and continues 256 -> 32 -> 4 -> per-round leaves, the best ladder of that sweep (231.7 ms per 1M window
   // against 240-259 for the others); the cost model below was fitted on sparser failures
-  if (dense && (gsize == 256 || gsize == 32)) return gsize == 256 ? 32 : 4;
-  if (dense && gsize == 4) return 1;
+  if (!tree && dense && (gsize == 256 || gsize == 32)) return gsize == 256 ? 32 : 4;
+  if (!tree && dense && gsize == 4) return 1;
   const double f = (double)nfail / (double)ngroups;
   const double per_group = nfail == ngroups ? 5.0 : -std::log1p(-f);
   const double faults = std::max((double)nfail, per_group * (double)ngroups);
   const double density = std::min(1.0, faults / (double)std::max<size_t>(m_next, 1));
   size_t g = 1;
-  descent_cost((double)m_next, density, gsize, &g);
+  descent_cost((double)m_next, density, gsize, &g, tree);
   return g;
+}
+
+// Bisection from scaled points (launch_scale28 once per batch, then launch_group_sums28 per level) instead of an MSM
+// per level; DRANDHIP_BISECT_TREE=0 keeps the per-level MSMs (the r03 path, for comparison)
+static bool tree_bisection() {
+  static const bool v = [] {
+    const char* e = getenv("DRANDHIP_BISECT_TREE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
 }
 
 // core pipeline on device-resident inputs
@@ -685,6 +701,11 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
 
   timed_launches T(st);
   bool presorted = false;  // level-0 sorted lists already built on the tail stream
+  // bisection from scaled points: from level 0 on when this worker's last bisection saw dense faults (> 1 per 2000
+  // rounds: its level 0 is expected to fail, and the scaled points give every level's sums), else once level 0 failed
+  const bool tree_ok = msm28 && tree_bisection();
+  const bool tree_first = tree_ok && mode <= VM_BEGIN && w->fault_density > 1.0 / 2000 && n > 4096;
+  bool tree = tree_first, scaled = false;
   dh::msm_geom g0{};
   dh::msm_ws ws0{};
   if (mode <= VM_BEGIN) {
@@ -704,8 +725,9 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
     // The level-0 sort needs only the scalars, and the scalars only the seed: with a tail stream it runs there
     // while the per-round kernels decode and hash (its ~1 ms of small kernels left the one-call latency path).
-    // Every round then carries a scalar; the bucket passes skip rounds whose status is not DEC_OK.
-    presorted = w->tail && st == w->stream;
+    // Every round then carries a scalar; the bucket passes skip rounds whose status is not DEC_OK. A worker whose
+    // last bisection saw dense faults takes level 0 from the scaled points instead (no sort).
+    presorted = w->tail && st == w->stream && !tree_first;
     if (presorted) {
       hipStream_t ts = w->tail;
       HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, ts));
@@ -791,11 +813,31 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     dh::msm_ws ws{};
     if (pre) {
       ws = ws0;
-    } else {
+    } else if (!tree) {  // (tree levels need no MSM workspace: a small-group geometry would size it for every group)
       const int rc = msm_workspace(w, g, m, ngroups, wsw, ws);
       if (rc) return rc;
     }
-    if (!(level == 0 && mode >= VM_FINISH)) {  // a resumed batch has its level-0 sums from dh_batch_begin
+    if (tree && !(level == 0 && mode >= VM_FINISH)) {
+      if (!scaled) {  // once per batch: [r_i] sigma_i and [r_i] H_i
+        HIP_TRY(w->tree_r.ensure(dh::scaled_points_bytes(g2, n)));
+        HIP_TRY(T.run("k_scale28", [&] {
+          return dh::launch_scale28(g2, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), w->s28.as<uint32_t>(),
+                                    w->q28.as<uint32_t>(), w->tree_r.as<uint32_t>(), st);
+        }));
+        scaled = true;
+      }
+      const size_t tb = dh::group_sums_tmp_bytes(g2, m, gsize);
+      HIP_TRY(w->tree_a.ensure(tb));
+      HIP_TRY(w->tree_b.ensure(tb));
+      HIP_TRY(w->outA.ensure(ngroups * jw * 4));
+      HIP_TRY(w->outB.ensure(ngroups * jw * 4));
+      HIP_TRY(w->pass.ensure(ngroups));
+      HIP_TRY(T.run(level == 0 ? "tree_sums_level0" : "tree_sums_bisect", [&] {
+        return dh::launch_group_sums28(g2, w->entries.as<uint32_t>(), m, gsize, w->tree_r.as<uint32_t>(), n,
+                                       w->tree_a.as<uint32_t>(), w->tree_b.as<uint32_t>(), w->outA.as<uint32_t>(),
+                                       w->outB.as<uint32_t>(), st);
+      }));
+    } else if (!(level == 0 && mode >= VM_FINISH)) {  // a resumed batch has its level-0 sums from dh_batch_begin
       // every level skips the rounds whose status is not DEC_OK (their scalars are nonzero after a presort)
       HIP_TRY(T.run(msm_names[std::min(level, 7)], [&] {
         if (msm28)
@@ -847,7 +889,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     std::swap(w->entries, w->entries_alt);
     const size_t m_prev = m;
     m = nfail * gsize - (last_pass ? 0 : ngroups * gsize - m_prev);  // only the last group may be short
-    gsize = fixed.empty() ? next_group_size(gsize, ngroups, nfail, m_prev, m, w->fault_density)
+    if (tree_ok && m > 1) tree = true;  // the levels below take their sums from the scaled points
+    gsize = fixed.empty() ? next_group_size(gsize, ngroups, nfail, m_prev, m, w->fault_density, tree)
                           : (size_t)(level - 1 < (int)fixed.size() ? fixed[level - 1] : 1);
   }
   if (m > 0) {

@@ -983,6 +983,190 @@ hipError_t launch_msm28(int sig_g2, const msm_geom& g, const uint32_t* entries, 
   return hipMemcpyAsync(outB, ws.out2 + ngroups * ow, bytes, hipMemcpyDeviceToDevice, st);
 }
 
+// ================================================================ bisection from per-round scaled points
+// A batch whose level-0 check fails is bisected: every later level needs, per group G of its compacted entries,
+// A_G = sum_{i in G} r_i sigma_i and B_G = sum_{i in G} r_i H_i with the level-0 scalars. Instead of a grouped Pippenger
+// MSM per level (whose per-group bucket reduction dominates at small groups: a 64-round group cost ~4x the per-round
+// work of level 0), the scaled points R_i = [r_i] sigma_i and T_i = [r_i] H_i are computed ONCE per batch (k_scale28,
+// one lane per point: a joint double-and-add over the endomorphism parts of r_i with NAF digits of each part, on the
+// same 28-bit lazy points and formulas as the MSM), and each level's sums are segmented additions over the entries
+// (k_gsum28 + k_rowsum28): ~1 point addition per entry per level. The sums are the same group elements the MSM
+// computes (sum over parts h of [part_h] endo^h(P)), so verdicts do not depend on the path.
+template <class C>
+DH_DEV uint64_t part_value(const uint4& s, int h) {
+  if constexpr (C::PARTS == 4) return h == 0 ? s.x : h == 1 ? s.y : h == 2 ? s.z : s.w;  // 31-bit parts
+  else return h ? ((uint64_t)s.w << 32 | s.z) : ((uint64_t)s.y << 32 | s.x);             // 63-bit halves
+}
+// non-adjacent form of k < 2^63 as two digit masks: digit i = +1 at pos bit i, -1 at neg bit i (from 3k: the NAF's
+// nonzero digits sit where 3k and k differ, shifted down one; positions 0..63)
+DH_DEV void naf_masks(uint64_t k, uint64_t& pos, uint64_t& neg) {
+  const uint64_t k2 = k << 1, lo = k + k2;
+  const uint64_t c = lo < k2 ? 1 : 0;  // bit 64 of 3k
+  pos = ((lo & ~k) >> 1) | (c << 63);
+  neg = (~lo & k) >> 1;
+}
+template <class C, bool EXACT>
+DH_DEV typename C::P scale_run(const uint32_t* __restrict__ pts, size_t n, size_t i, const uint64_t* pos, const uint64_t* neg,
+                               int top) {
+  typename C::P acc = C::inf();
+#pragma unroll 1
+  for (int b = top; b >= 0; b--) {
+    if (!acc.inf) acc = C::dbl(acc);
+#pragma unroll 1
+    for (int h = 0; h < C::PARTS; h++) {
+      const bool dp = (pos[h] >> b) & 1, dn = (neg[h] >> b) & 1;
+      if (dp || dn) {
+        const uint32_t* pt = pts + 2 * C::EW * (h * n + i);
+        typename C::E x, y;
+        ld28(x, pt);
+        ld28(y, pt + C::EW);
+        if (dn) y = C::neg(y);
+        acc = EXACT ? C::madd(acc, x, y) : C::madd_fast(acc, x, y);
+      }
+    }
+  }
+  return acc;
+}
+// R[t] for t < n: [r_t] sigma_t; R[n + i]: [r_i] H_i (lazy Jacobian, identity for a round whose status is not DEC_OK)
+template <class C>
+__global__ __launch_bounds__(256, C::OCC) void k_scale28(size_t n, const uint8_t* __restrict__ status, const uint4* __restrict__ scal,
+                                                         const uint32_t* __restrict__ S, const uint32_t* __restrict__ Q,
+                                                         uint32_t* __restrict__ R) {
+  const size_t t = gtid();
+  if (t >= 2 * n) return;
+  const size_t i = t < n ? t : t - n;
+  typename C::P acc = C::inf();
+  if (status[i] == DEC_OK) {
+    const uint4 s = scal[i];
+    uint64_t pos[C::PARTS], neg[C::PARTS], any = 0;
+#pragma unroll
+    for (int h = 0; h < C::PARTS; h++) {
+      naf_masks(part_value<C>(s, h), pos[h], neg[h]);
+      any |= pos[h] | neg[h];
+    }
+    if (any) {
+      const int top = 63 - __builtin_clzll(any);
+      const uint32_t* pts = t < n ? S : Q;
+      acc = scale_run<C, false>(pts, n, i, pos, neg, top);
+      if (C::poisoned(acc)) acc = scale_run<C, true>(pts, n, i, pos, neg, top);
+    }
+  }
+  stj28<C>(R, t, acc);
+}
+
+// level sums, pass 1: one lane per (set, group, chunk of up to L entries of the group); out row (set * ngroups + g),
+// column c, cpg columns per row
+template <class C, bool EXACT>
+DH_DEV typename C::P chunk_sum(const uint32_t* __restrict__ entries, size_t a, size_t b, const uint32_t* __restrict__ R,
+                               size_t base) {
+  typename C::P acc = C::inf();
+#pragma unroll 1
+  for (size_t e = a; e < b; e++) acc = C::template add_mem<EXACT>(acc, R + (size_t)3 * C::EW * (base + entries[e]));
+  return acc;
+}
+template <class C>
+__global__ __launch_bounds__(256, C::OCC) void k_gsum28(const uint32_t* __restrict__ entries, size_t m, size_t gsize,
+                                                        size_t ngroups, uint32_t L, uint32_t cpg, const uint32_t* __restrict__ R,
+                                                        size_t n, uint32_t* __restrict__ out) {
+  const size_t t = gtid();
+  const size_t per_set = ngroups * cpg;
+  if (t >= 2 * per_set) return;
+  const size_t set = t / per_set, r = t % per_set, g = r / cpg, c = r % cpg;
+  const size_t g0 = g * gsize, gend = min(m, g0 + gsize);
+  const size_t a = g0 + c * (size_t)L, b = min(gend, a + L);
+  typename C::P acc = C::inf();
+  if (a < b) {
+    acc = chunk_sum<C, false>(entries, a, b, R, set * n);
+    if (C::poisoned(acc)) acc = chunk_sum<C, true>(entries, a, b, R, set * n);
+  }
+  stj28<C>(out, t, acc);
+}
+// pass 2..: each lane adds up to `fan` consecutive columns of a row; the last pass (one column left) writes the
+// 12 x 32-bit Montgomery Jacobian the group checks read: rows < ngroups to outA, the others to outB
+template <class C, bool EXACT>
+DH_DEV typename C::P cols_sum(const uint32_t* __restrict__ in, size_t a, size_t b) {
+  typename C::P acc = ldj28<C>(in, a);
+#pragma unroll 1
+  for (size_t k = a + 1; k < b; k++) acc = C::template add_mem<EXACT>(acc, in + (size_t)3 * C::EW * k);
+  return acc;
+}
+template <class C>
+__global__ __launch_bounds__(256, C::OCC) void k_rowsum28(const uint32_t* __restrict__ in, size_t rows, uint32_t cnt, uint32_t fan,
+                                                          uint32_t* __restrict__ out, size_t ngroups, uint32_t* __restrict__ outA,
+                                                          uint32_t* __restrict__ outB) {
+  const size_t t = gtid();
+  const uint32_t cnt_out = (cnt + fan - 1) / fan;
+  if (t >= rows * cnt_out) return;
+  const size_t r = t / cnt_out, j = t % cnt_out;
+  const size_t a = r * cnt + j * (size_t)fan, b = r * cnt + min((size_t)cnt, (j + 1) * (size_t)fan);
+  typename C::P acc = cols_sum<C, false>(in, a, b);
+  if (C::poisoned(acc)) acc = cols_sum<C, true>(in, a, b);
+  if (cnt_out > 1) {
+    stj28<C>(out, t, acc);
+    return;
+  }
+  jac<typename C::F> q = jac_inf<typename C::F>();
+  if (!acc.inf) {
+    q.x = C::out(acc.x);
+    q.y = C::out(acc.y);
+    q.z = C::out(acc.z);
+  }
+  st_jac_aos<typename C::F>(r < ngroups ? outA : outB, r < ngroups ? r : r - ngroups, q);
+}
+
+size_t scaled_points_bytes(int sig_g2, size_t n) { return 2 * n * 3 * (sig_g2 ? 2 * W28 : W28) * 4; }
+
+hipError_t launch_scale28(int sig_g2, size_t n, const uint8_t* status, const uint4* scal, const uint32_t* S, const uint32_t* Q,
+                          uint32_t* R, hipStream_t st) {
+  if (!n) return hipSuccess;
+  if (sig_g2) hipLaunchKernelGGL(k_scale28<c28_g2>, dim3(nblk(2 * n, 256)), dim3(256), 0, st, n, status, scal, S, Q, R);
+  else hipLaunchKernelGGL(k_scale28<c28_g1>, dim3(nblk(2 * n, 256)), dim3(256), 0, st, n, status, scal, S, Q, R);
+  return hipGetLastError();
+}
+
+// chunk length of pass 1: about 2 x 131,072 lanes over both sets, at most 32 entries, within a group
+static uint32_t gsum_chunk(size_t m, size_t gsize) {
+  size_t L = 2 * m / 262144;
+  if (L < 1) L = 1;
+  if (L > 32) L = 32;
+  if (L > gsize) L = gsize;
+  return (uint32_t)L;
+}
+size_t group_sums_tmp_bytes(int sig_g2, size_t m, size_t gsize) {
+  const size_t ngroups = (m + gsize - 1) / gsize, L = gsum_chunk(m, gsize), cpg = (gsize + L - 1) / L;
+  return 2 * ngroups * cpg * 3 * (sig_g2 ? 2 * W28 : W28) * 4;
+}
+
+template <class C>
+static hipError_t group_sums28(const uint32_t* entries, size_t m, size_t gsize, const uint32_t* R, size_t n, uint32_t* tmpA,
+                               uint32_t* tmpB, uint32_t* outA, uint32_t* outB, hipStream_t st) {
+  const size_t ngroups = (m + gsize - 1) / gsize;
+  const uint32_t L = gsum_chunk(m, gsize);
+  uint32_t cnt = (uint32_t)((gsize + L - 1) / L);
+  const size_t rows = 2 * ngroups;
+  hipLaunchKernelGGL(k_gsum28<C>, dim3(nblk(rows * cnt, 256)), dim3(256), 0, st, entries, m, gsize, ngroups, L, cnt, R, n, tmpA);
+  uint32_t* in = tmpA;
+  uint32_t* out = tmpB;
+  for (;;) {
+    const uint32_t fan = 16, cnt_out = (cnt + fan - 1) / fan;
+    hipLaunchKernelGGL(k_rowsum28<C>, dim3(nblk(rows * cnt_out, 256)), dim3(256), 0, st, in, rows, cnt, fan, out, ngroups, outA,
+                       outB);
+    if (cnt_out == 1) break;
+    cnt = cnt_out;
+    uint32_t* sw = in;
+    in = out;
+    out = sw;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_group_sums28(int sig_g2, const uint32_t* entries, size_t m, size_t gsize, const uint32_t* R, size_t n,
+                               uint32_t* tmpA, uint32_t* tmpB, uint32_t* outA, uint32_t* outB, hipStream_t st) {
+  if (!m) return hipSuccess;
+  return sig_g2 ? group_sums28<c28_g2>(entries, m, gsize, R, n, tmpA, tmpB, outA, outB, st)
+                : group_sums28<c28_g1>(entries, m, gsize, R, n, tmpA, tmpB, outA, outB, st);
+}
+
 // bisection: the entries of the failing groups, in order, on the device (groups are runs of gsize consecutive entries,
 // only the last one partial, so a failing group's entries land at rank(group) * gsize + their offset in the group)
 __global__ void k_fail_flags(const uint8_t* __restrict__ pass, size_t ngroups, uint32_t* __restrict__ flags) {

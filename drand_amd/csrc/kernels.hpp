@@ -109,6 +109,15 @@ hipError_t launch_sum_partials(int sig_g2, const uint32_t* parts, size_t k, size
 hipError_t launch_node_mark(size_t n, uint8_t* res, const uint8_t* status, uint8_t* verdict, hipStream_t st);
 hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,
                               uint8_t* verdict, hipStream_t st);
+// bisection from per-round scaled points (k_msm.hip): R = 2n lazy Jacobian points ([r_i] sigma_i, then [r_i] H_i) of the
+// 28-bit points of launch_msm_prep28; then per level the group sums of the entries (groups of gsize consecutive
+// entries) into outA / outB (12 x 32-bit Jacobian), with two temporaries of group_sums_tmp_bytes
+size_t scaled_points_bytes(int sig_g2, size_t n);
+hipError_t launch_scale28(int sig_g2, size_t n, const uint8_t* status, const uint4* scal, const uint32_t* S, const uint32_t* Q,
+                          uint32_t* R, hipStream_t st);
+size_t group_sums_tmp_bytes(int sig_g2, size_t m, size_t gsize);
+hipError_t launch_group_sums28(int sig_g2, const uint32_t* entries, size_t m, size_t gsize, const uint32_t* R, size_t n,
+                               uint32_t* tmpA, uint32_t* tmpB, uint32_t* outA, uint32_t* outB, hipStream_t st);
 // bisection: out = the entries of the groups with pass == 0, in order; rank[ngroups] = the number of failing groups
 // (flags: ngroups words, rank: ngroups + 1, scan_tmp: launch_scan's)
 hipError_t launch_compact_failing(const uint32_t* entries, size_t m, size_t gsize, size_t ngroups, const uint8_t* pass,

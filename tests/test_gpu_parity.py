@@ -330,19 +330,22 @@ def test_one_lane_pairing_path(dh):
         assert v == [x["valid"] for x in neg[name]["cases"]], name
 
 
+@pytest.mark.parametrize("tree", ["1", "0"])
 @pytest.mark.parametrize("ladder", ["4096,256,16,2", "64"])
-def test_fixed_bisection_ladder(dh, ladder):
+def test_fixed_bisection_ladder(dh, ladder, tree):
     """The bisection is exact whatever the group sizes: a fixed ladder (DRANDHIP_BISECT, the r01 sizes with the
     c = 10 window geometry, and a single level of 64 before leaves) rejects exactly the corrupted rounds, as the
-    default expected-cost ladder does in the tests above."""
+    default expected-cost ladder does in the tests above — with the level sums taken from per-round scaled points
+    (tree "1", the default; the second quicknet call, after a dense first one, also takes level 0 from them) and from a
+    grouped MSM per level (tree "0"). The G2 statistics pin the sums themselves: exactly one failing group per level."""
     import subprocess
     import sys
-    env = dict(os.environ, DRANDHIP_BISECT=ladder)
+    env = dict(os.environ, DRANDHIP_BISECT=ladder, DRANDHIP_BISECT_TREE=tree)
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "fixed_ladder_check.py")],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     got = json.loads(r.stdout.strip().splitlines()[-1])
-    assert got["rejected"] == got["expected"] and len(got["expected"]) == 200
+    assert got["rejected"] == got["expected"] == got["rejected_again"] and len(got["expected"]) == 200
     # G2 with one forged round: every level of the ladder fails exactly its group, leaves = the last size
     levels, failed, leaves, rejected = got["g2_stats"]
     last = int(ladder.split(",")[-1])
