@@ -199,7 +199,6 @@ def main():
     d_rand = [torch.zeros((n, 32), dtype=torch.uint8, device=dev) for _ in range(S)]
     pbytes = lib.dh_partial_bytes(sch.id)
     d_part = [torch.zeros(pbytes, dtype=torch.uint8, device=dev) for _ in range(S)]
-    slot_streams = [torch.cuda.Stream(device=dev) for _ in range(S)]
     torch.cuda.synchronize()
     state = {"node_check": node_check}
 
@@ -220,21 +219,19 @@ def main():
 
         def retire():
             slot, h = pending.popleft()
-            with torch.cuda.stream(slot_streams[slot]):
-                h.finish()
-                bits.append(pack_bits(d_verdict[slot]))
+            h.finish()
+            bits.append(pack_bits(d_verdict[slot]))
 
         for k in range(k_steps):
             if len(pending) == streams:
                 retire()
             slot = k % streams
-            # each slot's begin / collective / check are ordered on the slot's own torch stream: an input-ordering
-            # event on one shared stream would also carry that stream's wait for the previous batch's record, and
-            # chain every batch's per-round kernels behind the previous batch's MSM (r04a: 14.2 M/s at 131k, 8 slots)
-            with torch.cuda.stream(slot_streams[slot]):
-                pending.append((slot, begin_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot],
-                                                       d_rand[slot], d_part[slot], world, None, stage_host=gloo,
-                                                       rank=rank)))
+            # the record, the collective and the check of a batch run on that batch's own library stream
+            # (dist.begin_node_batch): no stream shared by the batches carries a wait for another batch's record (r04a
+            # ordered them all through torch's current stream and chained every batch's per-round kernels behind the
+            # previous batch's MSM: 14.2 M/s at 131k rounds, 8 slots)
+            pending.append((slot, begin_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot], d_rand[slot],
+                                                   d_part[slot], world, None, stage_host=gloo, rank=rank)))
         while pending:
             retire()
         torch.cuda.synchronize()

@@ -50,6 +50,7 @@ SIGNATURES = {
     "dh_batch_begin": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_size_t, _P, _P, _c.c_size_t, _P, _c.c_size_t, _P,
                                   _c.c_size_t, _P, _P, _c.c_uint64, _P, _c.POINTER(_P), _P]),
     "dh_batch_check": (_c.c_int, [_P, _P, _c.c_size_t, _P]),
+    "dh_batch_stream": (_P, [_P]),
     "dh_check_partials": (_c.c_int, [_c.c_int, _c.c_char_p, _c.c_size_t, _P, _c.c_size_t, _c.POINTER(_c.c_int)]),
     "dh_batch_finish": (_c.c_int, [_P, _c.c_int, _P]),
     "dh_profile": (_c.c_int, [_c.c_int]),

@@ -1374,9 +1374,9 @@ int dh_verify_batch(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t
 
 // ---- node-wide batch check over several processes (one per GPU)
 // A node batch holds ONE worker from dh_batch_begin to dh_batch_finish and runs everything on it: the per-round
-// kernels on its stream, the level-0 MSM, the node-wide check of the gathered records and the bisection on its
-// high-priority tail stream. With a caller stream, nothing in begin / check waits on the host: the partial sums are
-// ordered onto the caller's stream (an event), the collective runs there, and the check is ordered after it.
+// kernels on its stream, the level-0 MSM, the record, the node-wide check of the gathered records and the bisection
+// on its high-priority tail stream (dh_batch_stream), where the caller also queues the collective. Nothing in begin
+// or check waits on the host, and with one rank nothing crosses streams at all.
 struct dh_batch {
   lease* L = nullptr;
   int scheme = 0;
@@ -1450,10 +1450,7 @@ int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t*
                     hipMemsetAsync(d_partials_out + 2 * jw * 4, 0, 16, ts) == hipSuccess;
     if (!ok) {
       rc = fail(DH_EDEVICE, "writing the partial sums failed");
-    } else if (hip_stream) {  // the caller's stream (the collective) is ordered after the record
-      if (hipEventRecord(w->part_ready, ts) != hipSuccess || hipStreamWaitEvent((hipStream_t)hip_stream, w->part_ready, 0) != hipSuccess)
-        rc = fail(DH_EDEVICE, "cannot order the caller's stream after the partial sums");
-    } else if (hipStreamSynchronize(ts) != hipSuccess) {
+    } else if (!hip_stream && hipStreamSynchronize(ts) != hipSuccess) {  // no caller stream: the record on return
       rc = fail(DH_EDEVICE, "hipStreamSynchronize failed");
     }
   }
@@ -1483,11 +1480,13 @@ static int queue_node_check(worker* w, bool g2, const uint8_t* pk, size_t pk_len
   return DH_OK;
 }
 
+void* dh_batch_stream(dh_batch* b) { return b ? (void*)b->L->w->tail : nullptr; }
+
 int dh_batch_check(dh_batch* b, const uint8_t* d_partials, size_t k, void* hip_stream) {
   if (!b || !d_partials || !k) return fail(DH_EINVAL, "bad node-check arguments");
   worker* w = b->L->w;
   const bool g2 = sig_on_g2(b->scheme);
-  if (hip_stream) {  // the gathered records are produced on the caller's stream
+  if (hip_stream && (hipStream_t)hip_stream != w->tail) {  // the gathered records are produced on the caller's stream
     HIP_TRY(hipEventRecord(w->gath_ready, (hipStream_t)hip_stream));
     HIP_TRY(hipStreamWaitEvent(w->tail, w->gath_ready, 0));
   }

@@ -236,9 +236,13 @@ __global__ __launch_bounds__(64) void k_partial_leaf(const uint32_t* __restrict_
 // sigma_j = sum_k lambda_{j,k} sigma_{sel[j,k]}: Straus over t points with shared doublings.
 // lam: per term the NAF masks of lambda (16 words); row set lam_set[j], or the round's own rows when lam_set is null.
 // LG_LANES lanes per round, each running Straus (shared doublings) over every LG_LANES-th term of the
-// interpolation sum sum_k lambda_k sigma_k; the partial sums meet in LDS and the first lane of the round adds
-// them. One lane per round left most of the chip idle at 10^4-10^5 rounds and ran 33 terms x 127 additions
-// serially; four lanes cut the per-round latency ~3.8x for ~6% more doublings.
+// interpolation sum sum_k lambda_k sigma_k; the partial sums meet in LDS and one lane of the round adds them. One
+// lane per round left most of the chip idle at 10^4-10^5 rounds and ran 33 terms x 127 additions serially; four lanes
+// cut the per-round latency ~3.8x for ~6% more doublings. A workgroup is LG_LANES waves over the same 64 rounds, wave q
+// running term lane q of each: rounds that selected the same signers (the usual case: the same nodes answer every
+// round) have the same lambdas, so all 64 lanes of a wave take the same digits and branches. r03 put the LG_LANES
+// lanes of a round side by side in ONE wave, whose lanes then followed LG_LANES different digit patterns and ran
+// every addition step up to LG_LANES times, diverged.
 constexpr int LG_LANES = 4, LG_MAXK = 9;  // terms per lane and pass (t <= 36: one pass)
 // G2: the chain on the lazily reduced 28-bit form (fp2_28.hpp), the MSM's fast mixed additions (no exceptional-case
 // tests); a chain that met an exceptional case ends with Z = 0 mod p and is run again with the exact 32-bit formulas
@@ -270,16 +274,15 @@ DH_DEV j228 lagrange_chain28(const uint32_t* __restrict__ L, int q, int c0, int 
   return acc;
 }
 template <class F>
-__global__ __launch_bounds__(64) void k_lagrange(const uint32_t* __restrict__ sel, const uint32_t* __restrict__ lam,
-                                                 const uint32_t* __restrict__ lam_set, const uint8_t* __restrict__ ok,
-                                                 int t, size_t n_rounds, const uint32_t* __restrict__ sig_aff,
-                                                 uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __restrict__ sel, const uint32_t* __restrict__ lam,
+                                                            const uint32_t* __restrict__ lam_set, const uint8_t* __restrict__ ok,
+                                                            int t, size_t n_rounds, const uint32_t* __restrict__ sig_aff,
+                                                            uint32_t* __restrict__ out) {
   constexpr int JW = sizeof(F) / 4 * 3;
-  __shared__ uint32_t part[64 * JW];
-  __shared__ uint32_t idxS[64][LG_MAXK], lpS[64][LG_MAXK], lnS[64][LG_MAXK];
-  const size_t tid = gtid();
-  const size_t j = tid / LG_LANES;
-  const int q = (int)(tid % LG_LANES);
+  __shared__ uint32_t part[(LG_LANES - 1) * 64 * JW];  // the partial sums of waves 1 .. LG_LANES - 1
+  __shared__ uint32_t idxS[64 * LG_LANES][LG_MAXK], lpS[64 * LG_LANES][LG_MAXK], lnS[64 * LG_LANES][LG_MAXK];
+  const int q = (int)(threadIdx.x / 64);  // term lane: wave-uniform
+  const size_t j = (size_t)blockIdx.x * 64 + threadIdx.x % 64;
   jac<F> acc = jac_inf<F>();
   if (j < n_rounds && ok[j]) {
     const uint32_t* L = lam + (lam_set ? (size_t)lam_set[j] : j) * t * 16;  // per term: NAF positive mask, negative mask
@@ -321,10 +324,10 @@ __global__ __launch_bounds__(64) void k_lagrange(const uint32_t* __restrict__ se
       acc = jac_add(acc, part_acc);
     }
   }
-  st_jac_aos<F>(part, threadIdx.x, acc);
+  if (q) st_jac_aos<F>(part, threadIdx.x - 64, acc);
   __syncthreads();
   if (q == 0 && j < n_rounds) {
-    for (int r = 1; r < LG_LANES; r++) acc = jac_add(acc, ld_jac_aos<F>(part, threadIdx.x + r));
+    for (int r = 1; r < LG_LANES; r++) acc = jac_add(acc, ld_jac_aos<F>(part, (size_t)(r - 1) * 64 + threadIdx.x));
     st_jac_aos<F>(out, j, acc);
   }
 }
@@ -432,10 +435,10 @@ hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam,
                            int t, size_t n_rounds, const uint32_t* sig_aff, uint32_t* out, hipStream_t st) {
   if (!n_rounds) return hipSuccess;
   if (sig_g2)
-    hipLaunchKernelGGL(k_lagrange<fp2>, dim3(nblk(n_rounds * LG_LANES, 64)), dim3(64), 0, st, sel, lam, lam_set, ok, t,
+    hipLaunchKernelGGL(k_lagrange<fp2>, dim3(nblk(n_rounds, 64)), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t,
                        n_rounds, sig_aff, out);
   else
-    hipLaunchKernelGGL(k_lagrange<fp>, dim3(nblk(n_rounds * LG_LANES, 64)), dim3(64), 0, st, sel, lam, lam_set, ok, t,
+    hipLaunchKernelGGL(k_lagrange<fp>, dim3(nblk(n_rounds, 64)), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t,
                        n_rounds, sig_aff, out);
   return hipGetLastError();
 }

@@ -179,6 +179,14 @@ def rank_seed(seed, rank):
     return int.from_bytes(h.digest()[:8], "little") or 1
 
 
+class _nullcontext:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
 def _status_offset(pb):
     """Byte offset of the status word in a partial record of pb bytes: [A | B | status | 3 pad words]."""
     return pb - 16
@@ -212,8 +220,9 @@ def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, pa
     """Begin one batch under the node-wide check and queue its exchange and check: dh_batch_begin
     (per-round kernels + level-0 MSM, record written into `partials`, a uint8 device tensor of dh_partial_bytes) ->
     all-gather of the records -> dh_batch_check (ONE pairing check of the summed records, on this batch's worker).
-    Under nccl the whole chain is queued without a host wait: the library orders torch's current stream (where the
-    collective runs) after the record, and its check after the collective. Under gloo (stage_host) the records go
+    The record, the collective and the check are queued in the order of the batch's own library stream
+    (dh_batch_stream, as a torch ExternalStream): under nccl nothing waits on the host, and with one rank nothing
+    crosses streams; the inputs are ordered after torch's current stream. Under gloo (stage_host) the records go
     through host memory. A rank whose dh_batch_begin failed still takes part in the exchange with a record whose
     status word is 1, so every rank's check sees it and abandons the batch (finish raises everywhere) instead of
     blocking in the collective. Returns a NodeBatch; its finish() waits for the verdicts."""
@@ -235,21 +244,27 @@ def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, pa
                             ctypes.byref(b), ptr(partials))
     err = None if rc == 0 else "rank %d: dh_batch_begin: %s" % (rank, _lib.last_error())
     pb = partials.numel()
-    if err is not None:  # this rank's record: identity sums, status word 1
-        partials.zero_()
-        partials[_status_offset(pb)] = 1
-    if world == 1:
-        gathered = partials
-    else:
-        if stage_host is None:
-            stage_host = not dist.get_backend(group) == "nccl"
-        slot = partials.cpu() if stage_host else partials
-        gathered = gather_partials(slot, world, group)
-        if stage_host:
-            gathered = gathered.to(partials.device)
+    # the record, the collective and the check in the order of the batch's own library stream (dh_batch_stream);
+    # a rank whose begin failed writes its record (identity sums, status word 1) on its current stream instead
+    ctx = stream
+    if err is None and partials.is_cuda:
+        ctx = torch.cuda.ExternalStream(lib.dh_batch_stream(b), device=partials.device)
+    with torch.cuda.stream(ctx) if ctx is not None else _nullcontext():
+        if err is not None:
+            partials.zero_()
+            partials[_status_offset(pb)] = 1
+        if world == 1:
+            gathered = partials
+        else:
+            if stage_host is None:
+                stage_host = not dist.get_backend(group) == "nccl"
+            slot = partials.cpu() if stage_host else partials
+            gathered = gather_partials(slot, world, group)
+            if stage_host:
+                gathered = gathered.to(partials.device)
     if err is not None:
         return NodeBatch(lib, None, None, err, rank)
-    rc = lib.dh_batch_check(b, ptr(gathered), world, sp)
+    rc = lib.dh_batch_check(b, ptr(gathered), world, None)  # queued on the batch's stream, after the gather
     if rc != 0:
         e = "rank %d: dh_batch_check: %s" % (rank, _lib.last_error())
         lib.dh_batch_finish(b, -1, None)
@@ -356,3 +371,36 @@ def replay_shard(lib, scheme, pk, first, last, sig_of, rank, world, group=None, 
         got = np.unpackbits(b_.cpu().numpy())[:z - a]
         faulty += [first + a + int(i) for i in np.flatnonzero(got == 0)]
     return faulty
+
+
+def recover_shard(scheme, commits, t, n, msgs, partials_per_round, rank, world, group=None):
+    """tbls Recover over the node (chain/beacon/chainstore.go:202-207, config 4 sharded as SURVEY.md §8e): the rounds
+    are split with shard_range, each rank recovers and verifies its own rounds on its GPU (dh_recover_batch: the
+    VerifyPartial batch check, selection, Lagrange interpolation and VerifyRecovered, all on the device), and the
+    recovered signatures and status flags are all-gathered, so every rank returns the whole node's (signatures
+    (n_rounds, sig_len) uint8, ok (n_rounds,) bool) in round order. Rounds are independent (each has its own partials
+    and message): no exchange before the gather. A rank whose recovery fails flags it in the gather (NodeFailure on
+    every rank)."""
+    import torch
+    lo, hi = shard_range(rank, world, len(msgs))
+    failed = None
+    sl = scheme.sig_len
+    sigs = np.zeros((hi - lo, sl), np.uint8)
+    ok = np.zeros(hi - lo, bool)
+    try:
+        if hi > lo:
+            sigs, ok = scheme.recover_batch(commits, t, n, msgs[lo:hi], partials_per_round[lo:hi])
+    except Exception as e:  # noqa: BLE001 - joined below, so no rank waits in the gather for this one
+        failed = "rank %d: Recover: %s" % (rank, e)
+    if world == 1:
+        if failed:
+            raise NodeFailure(failed)
+        return sigs, ok
+    dev = _collective_device(group)
+    rec = np.zeros((hi - lo, sl + 1), np.uint8)
+    rec[:, :sl] = sigs
+    rec[:, sl] = ok
+    flat = torch.from_numpy(rec.reshape(-1)).to(dev)
+    parts = gather_verdicts(flat, world, group, failed=failed)  # variable-size byte columns, failure flag included
+    out = np.concatenate([p.cpu().numpy().reshape(-1, sl + 1) for p in parts])
+    return np.ascontiguousarray(out[:, :sl]), out[:, sl].astype(bool)

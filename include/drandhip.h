@@ -166,11 +166,13 @@ int dh_verify_partials_batch(int scheme, const uint8_t* commits, int t, int n_no
  * shard's own level-0 check and bisection ran, so the verdicts are per-round exact either way), or DH_EABANDONED
  * (some rank's record carried a nonzero status: nothing is valid), or another error.
  *
- * Streams: with hip_stream (a hipStream_t, e.g. torch's current stream, on which the collective runs) non-NULL,
- * dh_batch_begin waits on hip_stream for the inputs, returns as soon as the batch is queued, and makes hip_stream
- * wait for the record; dh_batch_check makes the check wait for hip_stream's work (the gathered records). Neither
- * blocks on the host: the only host wait of a batch is in dh_batch_finish. With hip_stream NULL, dh_batch_begin
- * returns with the record written, and the gathered records must be complete when dh_batch_check is called.
+ * Streams: the batch's record is written, and its check and bisection run, on ONE stream of the library,
+ * dh_batch_stream(b) (a hipStream_t): the caller queues the collective there (e.g. torch.cuda.ExternalStream), so the
+ * record, the all-gather and the check follow each other in stream order, with no host wait and, for one rank, no
+ * cross-stream wait. With hip_stream (a hipStream_t) non-NULL, dh_batch_begin orders the batch after hip_stream's work
+ * (the inputs) and returns as soon as the batch is queued; with NULL it returns with the record written.
+ * dh_batch_check orders the check after hip_stream's work when hip_stream is another stream (the gathered records
+ * produced there); NULL or dh_batch_stream(b) adds no wait. The only host wait of a batch is in dh_batch_finish.
  *
  * A batch holds one library worker from begin to finish (DH_EBUSY if none is idle: begin never waits, since the
  * other ranks may be waiting in the collective); the arguments of dh_batch_begin must stay valid until
@@ -186,6 +188,7 @@ int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t*
                    size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
                    uint8_t* d_verdict_out, uint8_t* d_rand_out, uint64_t seed, void* hip_stream, dh_batch** batch_out,
                    uint8_t* d_partials_out);
+void* dh_batch_stream(dh_batch* batch);
 int dh_batch_check(dh_batch* batch, const uint8_t* d_partials, size_t k, void* hip_stream);
 int dh_check_partials(int scheme, const uint8_t* pk, size_t pk_len, const uint8_t* d_partials, size_t k, int* pass_out);
 int dh_batch_finish(dh_batch* batch, int node_pass, uint64_t stats_out[4]);

@@ -209,3 +209,84 @@ def test_node_batch_protocol_gloo(fail_rank):
         assert res[0]["seen"] == b"".join(recs) and res[fail_rank]["seen"] is None
     assert res[2]["gather"] == "boom" and all("rank(s) [2]" in m["gather"] for m in res[:2])
     assert rank_seed(0, 3) == 0
+
+
+# ---------------------------------------------------------------- sharded tbls Recover (config 4 over the node)
+class _OracleRecoverScheme:
+    """Stands in for drand_amd.scheme.Scheme.recover_batch on the CPU: the oracle's per-round Recover (kyber sign/tbls
+    restated), so recover_shard's sharding and gather run here without a GPU."""
+
+    def __init__(self, name, orc):
+        self.name, self.orc = name, orc
+        self.sig_len = 96 if name.startswith("pedersen") else 48
+
+    def recover_batch(self, commits, t, n, msgs, parts):
+        sigs = np.zeros((len(msgs), self.sig_len), np.uint8)
+        ok = np.zeros(len(msgs), bool)
+        for j, (m, ps) in enumerate(zip(msgs, parts)):
+            r = self.orc.recover(self.name, commits, t, n, m, ps)
+            if r is not None:
+                sigs[j] = np.frombuffer(r, np.uint8)
+                ok[j] = True
+        return sigs, ok
+
+
+def _tbls_case(orc, name, t, n, nr):
+    import hashlib
+    R = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    coeffs = [int.from_bytes(hashlib.sha256(b"shard-rec-%d" % j).digest(), "big") % R for j in range(t)]
+    commits = [orc.public_key(name, c.to_bytes(32, "big")) for c in coeffs]
+
+    def share(i):
+        x, acc = i + 1, 0
+        for cf in reversed(coeffs):
+            acc = (acc * x + cf) % R
+        return acc.to_bytes(32, "big")
+
+    msgs = [orc.digest_beacon(name, 100 + j) for j in range(nr)]
+    parts = []
+    for j in range(nr):
+        ids = [(j + k) % n for k in range(t if j % 3 else t - 1)]  # every third round: one partial short
+        parts.append([i.to_bytes(2, "big") + orc.sign(name, share(i), msgs[j]) for i in ids])
+    return commits, msgs, parts
+
+
+def _recover_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ctypes as orc
+    from drand_amd.dist import recover_shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    name = "pedersen-bls-unchained"
+    commits, msgs, parts = _tbls_case(orc, name, 3, 5, 7)
+    sigs, ok = recover_shard(_OracleRecoverScheme(name, orc), commits, 3, 5, msgs, parts, rank, world)
+    q.put({"rank": rank, "sigs": sigs.tobytes(), "ok": ok.tolist()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_recover_shard_gloo(oracle):
+    """recover_shard at world 3 (gloo, CPU; Recover itself on the oracle): every rank returns the whole node's
+    recovered signatures and status flags in round order, equal to a serial Recover of every round."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_recover_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    name = "pedersen-bls-unchained"
+    commits, msgs, parts = _tbls_case(oracle, name, 3, 5, 7)
+    want = [oracle.recover(name, commits, 3, 5, m, ps) for m, ps in zip(msgs, parts)]
+    for m in res:
+        assert m["ok"] == [w is not None for w in want]
+        got = np.frombuffer(m["sigs"], np.uint8).reshape(7, 96)
+        for j, w in enumerate(want):
+            if w is not None:
+                assert got[j].tobytes() == w
+    assert sum(m["ok"]) == 4  # rounds 0, 3, 6 are one partial short

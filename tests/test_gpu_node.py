@@ -144,7 +144,10 @@ def test_node_wide_check_all_schemes(dh, oracle, name, mode):
             assert rc == 0, _lib.last_error()
             handles.append(b)
         if mode == "device":
-            # the records are complete in the current stream's order: a copy queued there sees them
+            # each record is complete in its batch's stream order (dh_batch_stream): the current stream waits for all
+            # three, and each check is ordered after the current stream's work
+            for b in handles:
+                cur.wait_stream(torch.cuda.ExternalStream(lib.dh_batch_stream(b), device=dev))
             snap = parts.clone()
             results, stats = [], []
             for b in handles:
@@ -219,6 +222,8 @@ def test_node_batch_abandoned(dh):
     assert lib.dh_batch_begin(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr()), ctypes.c_void_p(d_s.data_ptr()), 48,
                               None, 0, None, n, ctypes.c_void_p(d_v.data_ptr()), None, 3, sp, ctypes.byref(b),
                               ctypes.c_void_p(parts.data_ptr())) == 0, _lib.last_error()
+    # the status byte was written on the current stream, the record on the batch's stream: the check is queued on the
+    # batch's stream after the current stream's work
     assert lib.dh_batch_check(b, ctypes.c_void_p(parts.data_ptr()), 2, sp) == 0, _lib.last_error()
     assert lib.dh_batch_finish(b, _lib.DH_NODE_CHECKED, None) == _lib.DH_EABANDONED
     torch.cuda.synchronize()
@@ -366,3 +371,78 @@ def test_bench_launches_ranks():
     bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True, text=True,
                          env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), timeout=120)
     assert bad.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in bad.stderr
+
+
+# ---------------------------------------------------------------- sharded tbls Recover, two processes
+def _recover_shard_worker(rank, world, port, name, commits, t, n, msgs, parts, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        sys.path.insert(0, ROOT)
+        from drand_amd import _lib, scheme_from_name
+        from drand_amd.dist import recover_shard
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        assert _lib.load().dh_init(1) == 0, _lib.last_error()
+        torch.cuda.set_device(0)
+        sigs, ok = recover_shard(scheme_from_name(name), commits, t, n, msgs, parts, rank, world)
+        q.put({"rank": rank, "sigs": sigs.tobytes(), "ok": ok.tolist()})
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        import traceback
+        q.put({"rank": rank, "error": repr(e) + traceback.format_exc()})
+
+
+def test_recover_shard_two_processes(dh, oracle):
+    """drand_amd.dist.recover_shard in two spawned processes (gloo, both on GPU 0, the real library): 40 rounds of a
+    16-signer, threshold-9 group split over the ranks, with rounds short of t valid partials and an invalid partial in
+    front; both ranks return the whole node's recovered signatures and flags, equal to the oracle's Recover per
+    round (kyber sign/tbls restated) and to the group signature [f(0)] H(m)."""
+    import random
+    import torch.multiprocessing as mp
+    name = "pedersen-bls-unchained"
+    s = dh.scheme_from_name(name)
+    n, t, nr, world = 16, 9, 40, 2
+    coeffs = [int.from_bytes(hashlib.sha256(b"rshard-%d" % j).digest(), "big") % R_ORDER for j in range(t)]
+    commits = [s.public_key(c.to_bytes(32, "big")) for c in coeffs]
+
+    def share(i):
+        x, acc = i + 1, 0
+        for cf in reversed(coeffs):
+            acc = (acc * x + cf) % R_ORDER
+        return acc.to_bytes(32, "big")
+
+    rounds = np.arange(900, 900 + nr, dtype=np.uint64)
+    shares = [s.sign_beacons(share(i), rounds) for i in range(n)]
+    msgs = [s.digest_beacon(int(r)) for r in rounds]
+    rng = random.Random(77)
+    parts = []
+    for j in range(nr):
+        ids = rng.sample(range(n), t - 1 if j % 5 == 0 else rng.randrange(t, n + 1))
+        ps = [i.to_bytes(2, "big") + shares[i][j].tobytes() for i in ids]
+        if j % 4 == 1:  # another round's signature in front
+            ps.insert(0, ids[0].to_bytes(2, "big") + shares[ids[0]][(j + 1) % nr].tobytes())
+        parts.append(ps)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_recover_shard_worker, args=(r, world, port, name, commits, t, n, msgs, parts, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [m["error"] for m in res if "error" in m]
+    assert not errs, errs
+    want = [oracle.recover(name, commits, t, n, m, ps) for m, ps in zip(msgs, parts)]
+    group = s.sign_beacons(coeffs[0].to_bytes(32, "big"), rounds)
+    for m in res:
+        assert m["ok"] == [w is not None for w in want]
+        got = np.frombuffer(m["sigs"], np.uint8).reshape(nr, 96)
+        for j, w in enumerate(want):
+            if w is not None:
+                assert got[j].tobytes() == w == group[j].tobytes()
+    assert sum(res[0]["ok"]) == nr - nr // 5
