@@ -231,7 +231,8 @@ def main():
             # ordered them all through torch's current stream and chained every batch's per-round kernels behind the
             # previous batch's MSM: 14.2 M/s at 131k rounds, 8 slots)
             pending.append((slot, begin_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot], d_rand[slot],
-                                                   d_part[slot], world, None, stage_host=gloo, rank=rank)))
+                                                   d_part[slot], world, None, stage_host=gloo, rank=rank,
+                                                   inputs_ready=True)))
         while pending:
             retire()
         torch.cuda.synchronize()

@@ -114,7 +114,7 @@ struct worker {
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
-      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den;
+      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_aff28, r_tbl;
   std::vector<uint8_t> h_verdict;
   // decoded group key cache: the same key is used for every batch of a chain
   uint8_t cached_key[96];
@@ -130,7 +130,7 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &node_sum, &node_res, &tree_r,
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_aff28, &r_tbl, &node_sum, &node_res, &tree_r,
                    &tree_a, &tree_b};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
@@ -1067,7 +1067,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   HIP_TRY(w->r_sel.ensure(n_rounds * (size_t)t * 4));
   HIP_TRY(w->r_key.ensure(n_rounds * (size_t)t * 4));
   HIP_TRY(w->r_den.ensure(n_rounds * (size_t)t * 32));
-  HIP_TRY(w->r_lam.ensure(n_rounds * (size_t)t * 64));
+  HIP_TRY(w->r_lam.ensure(n_rounds * (size_t)t * 48 * 4));  // k_recover.hip LAM_WORDS per term
   HIP_TRY(w->r_rok.ensure(n_rounds));
   HIP_TRY(w->r_sig.ensure(n_rounds * jw * 4));
   HIP_TRY(T.run("k_select_lagrange", [&] {
@@ -1076,9 +1076,18 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
                                       w->r_lam.as<uint32_t>(), w->r_rok.as<uint8_t>(), st);
   }));
   // 13. interpolation on the device
+  if (g2) {  // the partials' points in the 28-bit form, and their width-4 NAF tables, once per valid partial
+    HIP_TRY(w->r_aff28.ensure(np * 64 * 4 + 256));
+    HIP_TRY(w->r_tbl.ensure(np * 256 * 4 + 1024));
+    HIP_TRY(dh::launch_aff28_g2(w->r_paff.as<uint32_t>(), np, w->r_aff28.as<uint32_t>(), st));
+    HIP_TRY(T.run("k_wnaf_table", [&] {
+      return dh::launch_wnaf_table_g2(w->r_aff28.as<uint32_t>(), w->r_ok.as<uint8_t>(), np, w->r_tbl.as<uint32_t>(), st);
+    }));
+  }
   HIP_TRY(T.run("k_lagrange", [&] {
     return dh::launch_lagrange(g2, w->r_sel.as<uint32_t>(), w->r_lam.as<uint32_t>(), nullptr, w->r_rok.as<uint8_t>(), t,
-                               n_rounds, w->r_paff.as<uint32_t>(), w->r_sig.as<uint32_t>(), st);
+                               n_rounds, w->r_paff.as<uint32_t>(), g2 ? w->r_aff28.as<uint32_t>() : nullptr,
+                               g2 ? w->r_tbl.as<uint32_t>() : nullptr, w->r_sig.as<uint32_t>(), st);
   }));
   std::vector<uint8_t> rok(n_rounds, 0);
   HIP_TRY(hipMemcpyAsync(rok.data(), w->r_rok.p, n_rounds, hipMemcpyDeviceToHost, st));
@@ -1450,8 +1459,6 @@ int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t*
                     hipMemsetAsync(d_partials_out + 2 * jw * 4, 0, 16, ts) == hipSuccess;
     if (!ok) {
       rc = fail(DH_EDEVICE, "writing the partial sums failed");
-    } else if (!hip_stream && hipStreamSynchronize(ts) != hipSuccess) {  // no caller stream: the record on return
-      rc = fail(DH_EDEVICE, "hipStreamSynchronize failed");
     }
   }
   if (rc) {

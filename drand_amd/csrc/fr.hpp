@@ -115,6 +115,42 @@ DH_DEV void fr_to_words(const fr& a, uint32_t out[8]) {
 }
 
 // non-adjacent form of k < 2^255 (little-endian words) as positive / negative digit masks over 256 positions
+// width-4 NAF of a scalar w < 2^255 (little-endian words): digit b in nibble b (word b / 8, bits 4 (b % 8)), 0 = zero,
+// v in 1..4 = +(2v - 1), v in 9..12 = -(2(v - 8) - 1): odd digits in [-7, 7], each followed by at least three zeros
+// (k_lagrange's table holds P, 3P, 5P, 7P); 256 positions suffice for w < 2^255
+DH_DEV void fr_wnaf4(const uint32_t w[8], uint32_t* nib) {
+  uint32_t k[9];
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = w[i];
+  k[8] = 0;
+  uint32_t acc = 0;
+#pragma unroll 1
+  for (int b = 0; b < 256; b++) {
+    uint32_t v = 0;
+    if (k[0] & 1) {
+      int d = (int)(k[0] & 15);
+      if (d >= 8) d -= 16;
+      if (d > 0) {  // k -= d: clears the low four bits, no borrow
+        k[0] -= (uint32_t)d;
+        v = (uint32_t)(d + 1) / 2;
+      } else {  // k += -d: the low four bits carry out
+        unsigned c = (unsigned)(-d);
+#pragma unroll
+        for (int i = 0; i < 9; i++) k[i] = __builtin_addc(k[i], 0u, c, &c);
+        v = 8 + (uint32_t)(1 - d) / 2;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 31);
+    k[8] >>= 1;
+    acc |= v << (4 * (b & 7));
+    if ((b & 7) == 7) {
+      nib[b >> 3] = acc;
+      acc = 0;
+    }
+  }
+}
+
 DH_DEV void fr_naf_masks(const uint32_t w[8], uint32_t* pos, uint32_t* neg) {
   uint32_t k[9];
 #pragma unroll

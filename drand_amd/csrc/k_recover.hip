@@ -17,6 +17,8 @@
 
 namespace dh {
 
+constexpr int LAM_WORDS = 48;  // per Lagrange term: NAF pos mask (8 words), neg mask (8), width-4 NAF nibbles (32)
+
 __global__ void k_repack_partials(const uint8_t* __restrict__ raw, size_t n, int sig_len, uint8_t* __restrict__ sigs,
                                   uint32_t* __restrict__ idx) {
   size_t i = gtid();
@@ -121,8 +123,8 @@ __global__ __launch_bounds__(256) void k_ok_from_status(const uint8_t* __restric
 // share.RecoverCommit / xyCommit, restated in oracle/bls_oracle.c or_recover): the first t valid partials in arrival
 // order (Recover stops at t), sorted by share index (stable), duplicate indices dropped; fewer than t distinct ->
 // not recovered. Then lambda_k = prod_{m != k} x_m / (x_m - x_k) over x = index + 1 in F_r (one batch inversion),
-// written as NAF digit masks for k_lagrange. sel/key: t words per round; den: 8 t words per round (scratch);
-// lam: 16 t words per round.
+// written for k_lagrange as NAF digit masks (G1) and width-4 NAF nibbles (G2). sel/key: t words per round; den: 8 t words
+// per round (scratch); lam: LAM_WORDS (48) t words per round: per term pos mask (8), neg mask (8), nibbles (32).
 __global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restrict__ off, const uint8_t* __restrict__ ok,
                                                         const uint32_t* __restrict__ share_idx, int t, size_t n_rounds,
                                                         uint32_t* __restrict__ sel, uint32_t* __restrict__ key,
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restri
   }
   rok[j] = 1;
   uint32_t* D = den + j * (size_t)t * 8;
-  uint32_t* L = lam + j * (size_t)t * 16;
+  uint32_t* L = lam + j * (size_t)t * LAM_WORDS;
   // pass 1: numerators (into lam's second half), denominators (scratch), prefix products (into lam's first half)
   fr pre = fr_one();
   for (int k = 0; k < t; k++) {
@@ -172,8 +174,8 @@ __global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restri
       dk = fr_mul(dk, fr_sub(xm, xk));
     }
     for (int w = 0; w < 8; w++) {
-      L[16 * k + w] = pre.v[w];
-      L[16 * k + 8 + w] = num.v[w];
+      L[LAM_WORDS * k + w] = pre.v[w];
+      L[LAM_WORDS * k + 8 + w] = num.v[w];
       D[8 * k + w] = dk.v[w];
     }
     pre = fr_mul(pre, dk);
@@ -183,8 +185,8 @@ __global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restri
   for (int k = t - 1; k >= 0; k--) {
     fr pk, nk, dk;
     for (int w = 0; w < 8; w++) {
-      pk.v[w] = L[16 * k + w];
-      nk.v[w] = L[16 * k + 8 + w];
+      pk.v[w] = L[LAM_WORDS * k + w];
+      nk.v[w] = L[LAM_WORDS * k + 8 + w];
       dk.v[w] = D[8 * k + w];
     }
     const fr dinv = fr_mul(inv, pk);
@@ -193,9 +195,10 @@ __global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restri
     fr_to_words(fr_mul(nk, dinv), words);
     fr_naf_masks(words, pos, neg);
     for (int w = 0; w < 8; w++) {
-      L[16 * k + w] = pos[w];
-      L[16 * k + 8 + w] = neg[w];
+      L[LAM_WORDS * k + w] = pos[w];
+      L[LAM_WORDS * k + 8 + w] = neg[w];
     }
+    fr_wnaf4(words, L + LAM_WORDS * k + 16);
   }
 }
 
@@ -244,39 +247,123 @@ __global__ __launch_bounds__(64) void k_partial_leaf(const uint32_t* __restrict_
 // lanes of a round side by side in ONE wave, whose lanes then followed LG_LANES different digit patterns and ran
 // every addition step up to LG_LANES times, diverged.
 constexpr int LG_LANES = 4, LG_MAXK = 9;  // terms per lane and pass (t <= 36: one pass)
-// G2: the chain on the lazily reduced 28-bit form (fp2_28.hpp), the MSM's fast mixed additions (no exceptional-case
-// tests); a chain that met an exceptional case ends with Z = 0 mod p and is run again with the exact 32-bit formulas
+// G2: the chain on the lazily reduced 28-bit form (fp2_28.hpp) over width-4 NAF digits and each partial's table of
+// P, 3P, 5P, 7P (1/5 of the positions take an addition instead of 1/3), with the MSM's fast mixed additions (no
+// exceptional-case tests); a chain that met an exceptional case ends with Z = 0 mod p and runs again with the exact
+// formulas. G1 keeps the 32-bit Straus chain over the NAF masks.
+// the partial signatures' affine points in the 28-bit form, converted once per partial (k_aff28_g2) instead of at each
+// of the ~85 additions per term that read them: x.c0, x.c1, y.c0, y.c1, 16 words each (14 limbs + 2 pad)
+constexpr int A28_WORDS = 64;
+DH_DEV f28 ld_f28w(const uint32_t* p) {
+  f28 a;
+  const uint4* q = (const uint4*)p;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint4 t = q[i];
+    a.l[4 * i] = t.x;
+    a.l[4 * i + 1] = t.y;
+    if (4 * i + 2 < 14) a.l[4 * i + 2] = t.z;
+    if (4 * i + 3 < 14) a.l[4 * i + 3] = t.w;
+  }
+  return a;
+}
+DH_DEV void st_f28w(uint32_t* p, const f28& a) {
+  uint4* q = (uint4*)p;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    q[i] = make_uint4(a.l[4 * i], a.l[4 * i + 1], 4 * i + 2 < 14 ? a.l[4 * i + 2] : 0u, 4 * i + 3 < 14 ? a.l[4 * i + 3] : 0u);
+}
+__global__ __launch_bounds__(256) void k_aff28_g2(const uint32_t* __restrict__ pts, size_t n, uint32_t* __restrict__ out) {
+  const size_t i = gtid();
+  if (i >= n) return;
+  const aff<fp2> a = ld_aff_aos<fp2>(pts, i);
+  uint32_t* o = out + (size_t)A28_WORDS * i;
+  st_f28w(o, f28_from_fp(a.x.c0));
+  st_f28w(o + 16, f28_from_fp(a.x.c1));
+  st_f28w(o + 32, f28_from_fp(a.y.c0));
+  st_f28w(o + 48, f28_from_fp(a.y.c1));
+}
+hipError_t launch_aff28_g2(const uint32_t* pts, size_t n, uint32_t* out, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_aff28_g2, dim3(nblk(n, 256)), dim3(256), 0, st, pts, n, out);
+  return hipGetLastError();
+}
+
+// G2 width-4 NAF table per valid partial: P, 3P, 5P, 7P affine in the 28-bit form (WT x 64 words), from one
+// variable-time Fp2 inversion of the three Jacobian Z's (Montgomery's trick; public values). The partials reaching
+// k_lagrange decoded to subgroup points, so 2P, 3P, 5P, 7P are finite and distinct from the points added to them: the
+// exact formulas only guard the table of a partial that is never selected.
+constexpr int WT = 4, TBL_WORDS = WT * A28_WORDS;
+__global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restrict__ aff28, const uint8_t* __restrict__ ok,
+                                                       size_t n, uint32_t* __restrict__ tbl) {
+  const size_t e = gtid();
+  if (e >= n || !ok[e]) return;
+  const uint32_t* p = aff28 + (size_t)A28_WORDS * e;
+  const f228 px{ld_f28w(p), ld_f28w(p + 16)}, py{ld_f28w(p + 32), ld_f28w(p + 48)};
+  uint32_t* o = tbl + (size_t)TBL_WORDS * e;
+#pragma unroll
+  for (int w = 0; w < A28_WORDS; w += 4) *(uint4*)(o + w) = *(const uint4*)(p + w);
+  const j228 two = j228_dbl(j228{px, py, f2_one(), false});
+  j228 m[3];
+  m[0] = j228_madd<true>(two, px, py);  // 3P
+  m[1] = j228_add<true>(m[0], two);     // 5P
+  m[2] = j228_add<true>(m[1], two);     // 7P
+  const f228 z01 = f2_red(f2_mul(m[0].z, m[1].z));
+  const f228 z012 = f2_red(f2_mul(z01, m[2].z));
+  f228 inv = f2_from_fp2(fp2_inv_vt(f2_to_fp2(z012)));  // 1 / (z0 z1 z2)
+  f228 zi[3];
+  zi[2] = f2_red(f2_mul(inv, z01));
+  inv = f2_red(f2_mul(inv, m[2].z));                      // 1 / (z0 z1)
+  zi[1] = f2_red(f2_mul(inv, m[0].z));
+  zi[0] = f2_red(f2_mul(inv, m[1].z));
+#pragma unroll 1
+  for (int k = 0; k < 3; k++) {
+    const f228 z2 = f2_red(f2_sqr<2>(zi[k]));
+    const f228 x = f2_red(f2_mul(m[k].x, z2));
+    const f228 y = f2_red(f2_mul(m[k].y, f2_red(f2_mul(z2, zi[k]))));
+    uint32_t* ok2 = o + A28_WORDS * (k + 1);
+    st_f28w(ok2, x.c0);
+    st_f28w(ok2 + 16, x.c1);
+    st_f28w(ok2 + 32, y.c0);
+    st_f28w(ok2 + 48, y.c1);
+  }
+}
+hipError_t launch_wnaf_table_g2(const uint32_t* aff28, const uint8_t* ok, size_t n, uint32_t* tbl, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_wnaf_table_g2, dim3(nblk(n, 256)), dim3(256), 0, st, aff28, ok, n, tbl);
+  return hipGetLastError();
+}
+
+// the width-4 NAF Straus chain of one lane's terms over their tables (nibble words of the current 8 positions in nw)
 template <bool EXACT>
-DH_DEV j228 lagrange_chain28(const uint32_t* __restrict__ L, int q, int c0, int nc, const uint32_t* __restrict__ sig_aff,
-                             const uint32_t* idx, uint32_t* lp, uint32_t* ln) {
+DH_DEV j228 lagrange_wnaf28(const uint32_t* __restrict__ L, int q, int c0, int nc, const uint32_t* __restrict__ tbl,
+                            const uint32_t* idx, uint32_t* nw) {
   j228 acc = j228_inf();
 #pragma unroll 1
   for (int b = 255; b >= 0; b--) {
-    if ((b & 31) == 31)
-      for (int i = 0; i < nc; i++) {
-        const uint32_t* Lk = L + (size_t)(q + LG_LANES * (c0 + i)) * 16;
-        lp[i] = Lk[b >> 5];
-        ln[i] = Lk[8 + (b >> 5)];
-      }
-    acc = j228_dbl(acc);
+    if ((b & 7) == 7)
+      for (int i = 0; i < nc; i++) nw[i] = L[(size_t)(q + LG_LANES * (c0 + i)) * LAM_WORDS + 16 + (b >> 3)];
+    if (!acc.inf) acc = j228_dbl(acc);
 #pragma unroll 1
     for (int i = 0; i < nc; i++) {
-      const uint32_t pb = (lp[i] >> (b & 31)) & 1, nb = (ln[i] >> (b & 31)) & 1;
-      if (pb | nb) {
-        const aff<fp2> pt = ld_aff_aos<fp2>(sig_aff, idx[i]);
-        const f228 x = f2_from_fp2(pt.x);
-        f228 y = f2_from_fp2(pt.y);
-        if (nb) y = f2_neg3(y);
+      const uint32_t v = (nw[i] >> (4 * (b & 7))) & 15;
+      if (v) {
+        const uint32_t* pt = tbl + (size_t)TBL_WORDS * idx[i] + A28_WORDS * ((v & 7) - 1);
+        const f228 x{ld_f28w(pt), ld_f28w(pt + 16)};
+        f228 y{ld_f28w(pt + 32), ld_f28w(pt + 48)};
+        if (v & 8) y = f2_neg3(y);
         acc = j228_madd<EXACT>(acc, x, y);
       }
     }
   }
   return acc;
 }
+
 template <class F>
 __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __restrict__ sel, const uint32_t* __restrict__ lam,
                                                             const uint32_t* __restrict__ lam_set, const uint8_t* __restrict__ ok,
                                                             int t, size_t n_rounds, const uint32_t* __restrict__ sig_aff,
+                                                            const uint32_t* __restrict__ aff28, const uint32_t* __restrict__ tbl,
                                                             uint32_t* __restrict__ out) {
   constexpr int JW = sizeof(F) / 4 * 3;
   __shared__ uint32_t part[(LG_LANES - 1) * 64 * JW];  // the partial sums of waves 1 .. LG_LANES - 1
@@ -285,7 +372,7 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
   const size_t j = (size_t)blockIdx.x * 64 + threadIdx.x % 64;
   jac<F> acc = jac_inf<F>();
   if (j < n_rounds && ok[j]) {
-    const uint32_t* L = lam + (lam_set ? (size_t)lam_set[j] : j) * t * 16;  // per term: NAF positive mask, negative mask
+    const uint32_t* L = lam + (lam_set ? (size_t)lam_set[j] : j) * t * LAM_WORDS;  // per term: NAF masks, wNAF nibbles
     const uint32_t* S = sel + j * (size_t)t;
     const int nt = (t - q + LG_LANES - 1) / LG_LANES;  // terms of this lane: k = q + LG_LANES i
     // digit masks of the current 32-bit chunk and the point indices live in LDS (dynamic indices, no scratch)
@@ -297,17 +384,18 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
       for (int i = 0; i < nc; i++) idx[i] = S[q + LG_LANES * (c0 + i)];
       if constexpr (sizeof(F) == sizeof(fp2)) {
         // a poisoned chain (an exceptional case met by the fast additions) is recomputed by the exact 32-bit chain below
-        const j228 a28 = lagrange_chain28<false>(L, q, c0, nc, sig_aff, idx, lp, ln);
-        if (!j228_poisoned(a28)) {
-          if (!a28.inf) acc = jac_add(acc, jac<F>{f2_to_fp2(a28.x), f2_to_fp2(a28.y), f2_to_fp2(a28.z)});
-          continue;
-        }
+        // width-4 NAF over the partials' tables; a chain that met an exceptional case (poisoned) runs again with
+        // the exact formulas
+        j228 a28 = lagrange_wnaf28<false>(L, q, c0, nc, tbl, idx, lp);
+        if (j228_poisoned(a28)) a28 = lagrange_wnaf28<true>(L, q, c0, nc, tbl, idx, lp);
+        if (!a28.inf) acc = jac_add(acc, jac<F>{f2_to_fp2(a28.x), f2_to_fp2(a28.y), f2_to_fp2(a28.z)});
+        continue;
       }
       jac<F> part_acc = jac_inf<F>();
       for (int b = 255; b >= 0; b--) {
         if ((b & 31) == 31)
           for (int i = 0; i < nc; i++) {
-            const uint32_t* Lk = L + (size_t)(q + LG_LANES * (c0 + i)) * 16;
+            const uint32_t* Lk = L + (size_t)(q + LG_LANES * (c0 + i)) * LAM_WORDS;
             lp[i] = Lk[b >> 5];
             ln[i] = Lk[8 + (b >> 5)];
           }
@@ -432,14 +520,15 @@ hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const 
 }
 
 hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
-                           int t, size_t n_rounds, const uint32_t* sig_aff, uint32_t* out, hipStream_t st) {
+                           int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* aff28, const uint32_t* tbl,
+                           uint32_t* out, hipStream_t st) {
   if (!n_rounds) return hipSuccess;
   if (sig_g2)
     hipLaunchKernelGGL(k_lagrange<fp2>, dim3(nblk(n_rounds, 64)), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t,
-                       n_rounds, sig_aff, out);
+                       n_rounds, sig_aff, aff28, tbl, out);
   else
     hipLaunchKernelGGL(k_lagrange<fp>, dim3(nblk(n_rounds, 64)), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t,
-                       n_rounds, sig_aff, out);
+                       n_rounds, sig_aff, aff28, tbl, out);
   return hipGetLastError();
 }
 

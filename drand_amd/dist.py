@@ -216,14 +216,15 @@ class NodeBatch:
 
 
 def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, partials, world, group=None,
-                     d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=None, rank=None):
+                     d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=None, rank=None,
+                     inputs_ready=False):
     """Begin one batch under the node-wide check and queue its exchange and check: dh_batch_begin
     (per-round kernels + level-0 MSM, record written into `partials`, a uint8 device tensor of dh_partial_bytes) ->
     all-gather of the records -> dh_batch_check (ONE pairing check of the summed records, on this batch's worker).
     The record, the collective and the check are queued in the order of the batch's own library stream
     (dh_batch_stream, as a torch ExternalStream): under nccl nothing waits on the host, and with one rank nothing
-    crosses streams; the inputs are ordered after torch's current stream. Under gloo (stage_host) the records go
-    through host memory. A rank whose dh_batch_begin failed still takes part in the exchange with a record whose
+    crosses streams; the inputs are ordered after torch's current stream (unless inputs_ready). Under gloo
+    (stage_host) the records go through host memory. A rank whose dh_batch_begin failed still takes part in the exchange with a record whose
     status word is 1, so every rank's check sees it and abandons the batch (finish raises everywhere) instead of
     blocking in the collective. Returns a NodeBatch; its finish() waits for the verdicts."""
     import torch
@@ -237,7 +238,10 @@ def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, pa
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
     stream = torch.cuda.current_stream(partials.device) if partials.is_cuda else None
-    sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None else None
+    # inputs still in production on the current stream are waited for; resident inputs (inputs_ready: the bench) are
+    # not, since the current stream also carries the earlier batches' verdict packing, queued behind other batches'
+    # saturating kernels (r04c: ordering on it cost the 131k-round node shape ~20%)
+    sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None and not inputs_ready else None
     b = ctypes.c_void_p()
     rc = lib.dh_batch_begin(scheme.id, pk, len(pk), ptr(d_rounds), ptr(d_sigs), scheme.sig_len, ptr(d_prevs),
                             prev_stride, ptr(d_prev_lens), n, ptr(d_verdict), ptr(d_rand), rank_seed(seed, rank), sp,

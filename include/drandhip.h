@@ -169,8 +169,9 @@ int dh_verify_partials_batch(int scheme, const uint8_t* commits, int t, int n_no
  * Streams: the batch's record is written, and its check and bisection run, on ONE stream of the library,
  * dh_batch_stream(b) (a hipStream_t): the caller queues the collective there (e.g. torch.cuda.ExternalStream), so the
  * record, the all-gather and the check follow each other in stream order, with no host wait and, for one rank, no
- * cross-stream wait. With hip_stream (a hipStream_t) non-NULL, dh_batch_begin orders the batch after hip_stream's work
- * (the inputs) and returns as soon as the batch is queued; with NULL it returns with the record written.
+ * cross-stream wait. dh_batch_begin returns as soon as the batch is queued; with hip_stream (a hipStream_t) non-NULL
+ * it orders the batch after hip_stream's work (inputs still in production there), with NULL the inputs must be
+ * complete. A host caller that wants the record itself waits for dh_batch_stream(b).
  * dh_batch_check orders the check after hip_stream's work when hip_stream is another stream (the gathered records
  * produced there); NULL or dh_batch_stream(b) adds no wait. The only host wait of a batch is in dh_batch_finish.
  *
