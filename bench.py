@@ -216,11 +216,17 @@ def main():
         `streams` are queued. One thread issues every rank's collectives in the same order over one process group."""
         pending = collections.deque()
         bits = []
+        ht = state.setdefault("node_host_s", collections.Counter())
 
         def retire():
             slot, h = pending.popleft()
+            t0 = time.perf_counter()
             h.finish()
+            t1 = time.perf_counter()
             bits.append(pack_bits(d_verdict[slot]))
+            ht["finish_wait"] += t1 - t0
+            ht["pack"] += time.perf_counter() - t1
+            ht["batches"] += 1
 
         for k in range(k_steps):
             if len(pending) == streams:
@@ -230,9 +236,11 @@ def main():
             # (dist.begin_node_batch): no stream shared by the batches carries a wait for another batch's record (r04a
             # ordered them all through torch's current stream and chained every batch's per-round kernels behind the
             # previous batch's MSM: 14.2 M/s at 131k rounds, 8 slots)
+            t0 = time.perf_counter()
             pending.append((slot, begin_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot], d_rand[slot],
                                                    d_part[slot], world, None, stage_host=gloo, rank=rank,
                                                    inputs_ready=True)))
+            ht["begin_exchange_check"] += time.perf_counter() - t0
         while pending:
             retire()
         torch.cuda.synchronize()
@@ -279,6 +287,7 @@ def main():
     warm_batches = max(args.warmup, S) if args.warmup else 0
     run_steps(warm_batches, S)
     lib.dh_profile(0 if args.no_stage_times else 1)
+    state["node_host_s"] = collections.Counter()  # the timed region's host time per pipeline phase
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -298,6 +307,7 @@ def main():
     # different batches share the CUs, so per-launch durations there are not one kernel's speed. Single-stream
     # local batches give each kernel the whole GPU; the dominant kernel's roofline comes from their HIP events (on
     # the library's stream). bench/profile.sh records the rocprofv3 kernel trace of the same batches.
+    node_host = dict(state.get("node_host_s", {}))
     state["node_check"] = False
     prof1 = {}
     if args.roofline_steps:
@@ -399,6 +409,8 @@ def main():
         "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in prof.items()},
         "stages_ms_single_stream": {k: round(v["total_ms"] / max(1, v["count"]), 3) for k, v in prof1.items()},
         "single_call": single,
+        "node_host_ms_per_batch": ({k: round(v * 1000 / node_host["batches"], 3) for k, v in node_host.items()
+                                    if k != "batches"} if node_host.get("batches") else None),
         "sign_seconds": round(t_sign, 2),
     }
     if world == 1 and not args.no_cpu_baseline:

@@ -114,7 +114,7 @@ struct worker {
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
-      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_aff28, r_tbl;
+      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_aff28, r_tbl, r_rstat;
   std::vector<uint8_t> h_verdict;
   // decoded group key cache: the same key is used for every batch of a chain
   uint8_t cached_key[96];
@@ -130,7 +130,7 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_aff28, &r_tbl, &node_sum, &node_res, &tree_r,
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_aff28, &r_tbl, &r_rstat, &node_sum, &node_res, &tree_r,
                    &tree_a, &tree_b};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
@@ -969,7 +969,10 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   HIP_TRY(hipMemcpyAsync(w->r_off.p, off_rel.data(), (n_rounds + 1) * 4, hipMemcpyHostToDevice, st));
   HIP_TRY(dh::launch_partial_meta(w->r_off.as<uint32_t>(), n_rounds, w->r_pidx.as<uint32_t>(), n_nodes,
                                   w->r_round_of.as<uint32_t>(), w->r_pstatus.as<uint8_t>(), st));
-  // 7. RLC scalars per partial (0 for partials that failed decoding or lie outside the group)
+  // 7. RLC scalars per partial (0 for partials that failed decoding or lie outside the group), split as the 28-bit MSM
+  // takes them: four 31-bit psi parts (G2 signatures) or two 63-bit phi halves (G1)
+  const int parts = g2 ? 4 : 2;
+  const size_t pw28 = g2 ? 64 : 32, wsw = g2 ? 96 : 48;  // words per 28-bit affine point / workspace Jacobian point
   uint32_t seedw[8];
   int rc = make_seed(0, seedw);
   if (rc) return rc;
@@ -977,7 +980,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
   HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
   HIP_TRY(w->r_scal.ensure(std::max(np, n_rounds) * 16 + 16));
-  HIP_TRY(dh::launch_scalars(d_seed, np, w->r_pstatus.as<uint8_t>(), w->r_scal.as<uint4>(), 0, st));
+  HIP_TRY(dh::launch_scalars(d_seed, np, w->r_pstatus.as<uint8_t>(), w->r_scal.as<uint4>(), parts, st));
   HIP_TRY(hipStreamSynchronize(st));
   for (int c = 0; c < t; c++)
     if (cst[c] != 1) return fail(DH_EKEY, "public polynomial commitment %d does not decode to a subgroup point", c);
@@ -991,37 +994,39 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), np, st));
     HIP_TRY(w->r_e_grp.ensure(np * 4 + 4));
     HIP_TRY(dh::launch_clamp_group(w->r_pidx.as<uint32_t>(), np, (uint32_t)n_nodes - 1, w->r_e_grp.as<uint32_t>(), st));
-    const dh::msm_geom gA = geom_for(std::max<size_t>(np, 1));
+    // the partials' sigmas and the rounds' hash points in the 28-bit form with their endomorphism images (a hash point
+    // at infinity, probability ~2^-255, leaves its round's slot unwritten: the batch check then fails and the partials
+    // get their leaf checks on the 32-bit points)
+    HIP_TRY(w->s28.ensure(parts * std::max<size_t>(np, 1) * pw28 * 4));
+    HIP_TRY(w->q28.ensure(parts * n_rounds * pw28 * 4));
+    HIP_TRY(w->r_rstat.ensure(n_rounds));
+    HIP_TRY(hipMemsetAsync(w->r_rstat.p, 1 /* DEC_OK */, n_rounds, st));
+    HIP_TRY(dh::launch_msm_prep28(g2, np, w->r_pstatus.as<uint8_t>(), w->r_paff.as<uint32_t>(), nullptr, w->s28.as<uint32_t>(),
+                                  nullptr, st, 1));
+    HIP_TRY(dh::launch_msm_prep28(g2, n_rounds, w->r_rstat.as<uint8_t>(), nullptr, w->r_q.as<uint32_t>(), nullptr,
+                                  w->q28.as<uint32_t>(), st, 2));
+    dh::msm_geom gA = geom_for(std::max<size_t>(np, 1), parts);
+    gA.half_stride = (uint32_t)np;
     size_t avg = std::max<size_t>(1, np / std::max(1, n_nodes));
-    dh::msm_geom gB = geom_for(avg);
-    while (gB.c > 3 && (size_t)n_nodes * gB.nwin * gB.nbuck > ((size_t)1 << 24)) gB = geom_for(((size_t)1 << (gB.c + 1)));
-    const size_t nkA = (size_t)gA.nwin * gA.nbuck, nkB = (size_t)n_nodes * gB.nwin * gB.nbuck;
-    const size_t nk = std::max(nkA, nkB);
-    HIP_TRY(w->cnt.ensure(nk * 4));
-    HIP_TRY(w->off.ensure((nk + 1) * 4));
-    HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
-    HIP_TRY(w->list.ensure(std::max(np * gA.nwin, np * gB.nwin) * 4 + 4));
-    HIP_TRY(w->buckets.ensure(nk * jw * 4));
-    HIP_TRY(w->segs.ensure(std::max((size_t)gA.nwin * gA.nseg, (size_t)n_nodes * gB.nwin * gB.nseg) * jw * 4));
+    dh::msm_geom gB = geom_for(avg, parts);
+    while (gB.c > 3 && (size_t)n_nodes * gB.nwin * gB.nbuck > ((size_t)1 << 24))
+      gB = geom_for(std::max<size_t>(1, ((size_t)1 << (gB.c + 1)) / parts), parts);
+    gB.half_stride = (uint32_t)n_rounds;
+    // one workspace for both (sized for each before anything is queued on it), used one MSM after the other
+    dh::msm_ws wsA{}, wsB{};
+    int rcw = msm_workspace(w, gA, np, 1, wsw, wsA);
+    if (!rcw) rcw = msm_workspace(w, gB, np, n_nodes, wsw, wsB);
+    if (!rcw) rcw = msm_workspace(w, gA, np, 1, wsw, wsA);
+    if (rcw) return rcw;
     HIP_TRY(w->outA.ensure(jw * 4));
     HIP_TRY(w->outB.ensure((size_t)n_nodes * jw * 4));
-    // chunk length depends on the list length: size for each of the two MSMs, not for the longer list
-    const size_t entA = np * gA.nwin, entB = np * gB.nwin;
-    HIP_TRY(w->part.ensure(std::max(dh::msm_part_bytes(entA, jw, 1), dh::msm_part_bytes(entB, jw, 1))));
-    HIP_TRY(w->meta.ensure(std::max(dh::msm_meta_bytes(entA), dh::msm_meta_bytes(entB))));
-    dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
-                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), nullptr, w->part.as<uint32_t>(),
-                  w->meta.as<uint32_t>(), 0};
     HIP_TRY(T.run("recover_msm_sigs", [&] {
-      hipError_t e = dh::launch_msm_sort(gA, w->entries.as<uint32_t>(), nullptr, nullptr, np, 1, w->r_scal.as<uint4>(), ws, st);
-      if (e != hipSuccess) return e;
-      return dh::launch_msm_points(g2, 1, gA, 1, w->r_paff.as<uint32_t>(), ws, w->outA.as<uint32_t>(), st);
+      return dh::launch_msm28_set(g2, gA, w->entries.as<uint32_t>(), nullptr, nullptr, np, 1, w->r_scal.as<uint4>(),
+                                  w->s28.as<uint32_t>(), wsA, w->outA.as<uint32_t>(), st);
     }));
     HIP_TRY(T.run("recover_msm_hash_by_signer", [&] {
-      hipError_t e = dh::launch_msm_sort(gB, w->r_round_of.as<uint32_t>(), w->entries.as<uint32_t>(), w->r_e_grp.as<uint32_t>(),
-                                         np, n_nodes, w->r_scal.as<uint4>(), ws, st);
-      if (e != hipSuccess) return e;
-      return dh::launch_msm_points(g2, 0, gB, n_nodes, w->r_q.as<uint32_t>(), ws, w->outB.as<uint32_t>(), st);
+      return dh::launch_msm28_set(g2, gB, w->r_round_of.as<uint32_t>(), w->entries.as<uint32_t>(), w->r_e_grp.as<uint32_t>(),
+                                  np, n_nodes, w->r_scal.as<uint4>(), w->q28.as<uint32_t>(), wsB, w->outB.as<uint32_t>(), st);
     }));
     // 10. multi-pairing: n_nodes + 1 pairs
     const size_t npairs = (size_t)n_nodes + 1;
@@ -1105,30 +1110,25 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     HIP_TRY(dh::launch_prep(g2, w->r_sigbytes.as<uint8_t>(), sl, n_rounds, w->r_status2.as<uint8_t>(),
                             w->r_aff2.as<uint32_t>(), nullptr, st));
     HIP_TRY(w->r_scal.ensure(std::max(np, n_rounds) * 16 + 16));  // rounds may outnumber the partials
-    HIP_TRY(dh::launch_scalars(d_seed, n_rounds, w->r_status2.as<uint8_t>(), w->r_scal.as<uint4>(), 0, st));
+    HIP_TRY(dh::launch_scalars(d_seed, n_rounds, w->r_status2.as<uint8_t>(), w->r_scal.as<uint4>(), parts, st));
     HIP_TRY(dh::launch_iota(w->r_entries2.as<uint32_t>(), n_rounds, st));
     // group key = commit 0 (affine, key group) — staged where the group check expects it
     HIP_TRY(w->key_aff.ensure(96 * 4));
     HIP_TRY(hipMemcpyAsync(w->key_aff.p, w->r_caff.p, kaw * 4, hipMemcpyDeviceToDevice, st));
     w->cached_key_len = 0;  // key_aff now holds this call's key
-    const dh::msm_geom g = geom_for(n_rounds);
-    const size_t nk = (size_t)g.nwin * g.nbuck;
-    HIP_TRY(w->cnt.ensure(nk * 4));
-    HIP_TRY(w->off.ensure((nk + 1) * 4));
-    HIP_TRY(w->scan_tmp.ensure(((nk + 4095) / 4096 + 1) * 4));
-    HIP_TRY(w->list.ensure(n_rounds * g.nwin * 4));
-    HIP_TRY(w->buckets.ensure(2 * nk * jw * 4));
-    HIP_TRY(w->segs.ensure(2 * (size_t)g.nwin * g.nseg * jw * 4));
-    HIP_TRY(w->out2.ensure(2 * jw * 4));
-    HIP_TRY(w->part.ensure(dh::msm_part_bytes(n_rounds * g.nwin, jw, 2)));
-    HIP_TRY(w->meta.ensure(dh::msm_meta_bytes(n_rounds * g.nwin)));
-    dh::msm_ws ws{w->cnt.as<uint32_t>(), w->off.as<uint32_t>(), w->scan_tmp.as<uint32_t>(), w->list.as<uint32_t>(),
-                  w->buckets.as<uint32_t>(), w->segs.as<uint32_t>(), w->out2.as<uint32_t>(), w->part.as<uint32_t>(),
-                  w->meta.as<uint32_t>(), 0};
+    dh::msm_geom g = geom_for(n_rounds, parts);
+    g.half_stride = (uint32_t)n_rounds;
+    dh::msm_ws ws{};
+    int rcw = msm_workspace(w, g, n_rounds, 1, wsw, ws);
+    if (rcw) return rcw;
+    HIP_TRY(w->s28.ensure(parts * n_rounds * pw28 * 4));
+    HIP_TRY(w->q28.ensure(parts * n_rounds * pw28 * 4));
+    HIP_TRY(dh::launch_msm_prep28(g2, n_rounds, w->r_status2.as<uint8_t>(), w->r_aff2.as<uint32_t>(), w->r_q.as<uint32_t>(),
+                                  w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), st));
     HIP_TRY(T.run("recover_verify", [&] {
-      hipError_t e = dh::launch_msm(g2, g, w->r_entries2.as<uint32_t>(), n_rounds, 1, w->r_scal.as<uint4>(),
-                                    w->r_aff2.as<uint32_t>(), w->r_q.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
-                                    w->outB.as<uint32_t>(), st);
+      hipError_t e = dh::launch_msm28(g2, g, w->r_entries2.as<uint32_t>(), n_rounds, 1, w->r_scal.as<uint4>(),
+                                      w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
+                                      w->outB.as<uint32_t>(), st, w->r_status2.as<uint8_t>(), false);
       if (e != hipSuccess) return e;
       return group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), 1, w->key_aff.as<uint32_t>(),
                          w->pass.as<uint8_t>(), st);

@@ -661,10 +661,12 @@ static uint32_t prep28_k(size_t n) {
   while (k < PREP28_KMAX && n / (2 * k) >= 131072) k *= 2;
   return k;
 }
+// sets: bit 0 converts S (sig_aff), bit 1 Q (q_pts); tbls Recover converts its partials and its round hash points
+// separately (different counts)
 template <class C>
 __global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint32_t K, uint8_t* __restrict__ status,
                                                        const uint32_t* __restrict__ sig_aff, const uint32_t* __restrict__ q_pts,
-                                                       uint32_t* __restrict__ S, uint32_t* __restrict__ Q) {
+                                                       uint32_t* __restrict__ S, uint32_t* __restrict__ Q, uint32_t sets) {
   using E = typename C::E;
   using F = typename C::F;
   constexpr int EW = C::EW, FW = npw<F>::N;
@@ -672,7 +674,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint32_t K, uin
   if (lo >= n) return;
   const size_t hi = min(n, lo + K);
 #pragma unroll 1
-  for (size_t i = lo; i < hi; i++) {
+  for (size_t i = lo; i < hi && (sets & 1); i++) {
     if (status[i] != DEC_OK) continue;
     const aff<F> a = ld_aff_aos<F>(sig_aff, i);
     const E x = C::in(a.x), y = C::in(a.y);
@@ -680,6 +682,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint32_t K, uin
     st28(S + 2 * EW * i + EW, y, 0);
     prep28_images<C>(S, n, i, x, y);
   }
+  if (!(sets & 2)) return;
   E acc = C::one();
   bool any = false;
 #pragma unroll 1
@@ -928,18 +931,21 @@ __global__ __launch_bounds__(64) void k_msm_windows28(const uint32_t* __restrict
 }
 
 hipError_t launch_msm_prep28(int sig_g2, size_t n, uint8_t* status, const uint32_t* sig_aff, const uint32_t* q_pts,
-                             uint32_t* S, uint32_t* Q, hipStream_t st) {
+                             uint32_t* S, uint32_t* Q, hipStream_t st, uint32_t sets) {
   if (!n) return hipSuccess;
   const uint32_t K = prep28_k(n);
   const size_t nt = (n + K - 1) / K;
-  if (sig_g2) hipLaunchKernelGGL(k_msm_prep28<c28_g2>, dim3(nblk(nt, 256)), dim3(256), 0, st, n, K, status, sig_aff, q_pts, S, Q);
-  else hipLaunchKernelGGL(k_msm_prep28<c28_g1>, dim3(nblk(nt, 256)), dim3(256), 0, st, n, K, status, sig_aff, q_pts, S, Q);
+  if (sig_g2)
+    hipLaunchKernelGGL(k_msm_prep28<c28_g2>, dim3(nblk(nt, 256)), dim3(256), 0, st, n, K, status, sig_aff, q_pts, S, Q, sets);
+  else
+    hipLaunchKernelGGL(k_msm_prep28<c28_g1>, dim3(nblk(nt, 256)), dim3(256), 0, st, n, K, status, sig_aff, q_pts, S, Q, sets);
   return hipGetLastError();
 }
 
+// nsets = 2: the sigma points S and the hash points Q share the sorted lists (the batch check); 1: S only
 template <class C>
 static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, const uint32_t* Q, msm_ws& ws, hipStream_t st,
-                        const uint8_t* skip) {
+                        const uint8_t* skip, int nsets = 2) {
   const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
   constexpr size_t jw = 3 * C::EW;
   uint32_t* bB = ws.buckets + nk * jw;
@@ -952,11 +958,13 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     hipLaunchKernelGGL((k_msm_bucket28<C, true>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, S, ws.buckets,
                        ws.part, ws.meta, skip, g.half_stride);
     hipLaunchKernelGGL(k_msm_bucket_fix28<C>, dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, nk, L, ws.meta, ws.part, ws.buckets);
-    hipLaunchKernelGGL((k_msm_bucket28<C, true>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, Q, bB, pB,
-                       ws.meta, skip, g.half_stride);
-    hipLaunchKernelGGL(k_msm_bucket_fix28<C>, dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, nk, L, ws.meta, pB, bB);
+    if (nsets == 2) {
+      hipLaunchKernelGGL((k_msm_bucket28<C, true>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, Q, bB, pB,
+                         ws.meta, skip, g.half_stride);
+      hipLaunchKernelGGL(k_msm_bucket_fix28<C>, dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, nk, L, ws.meta, pB, bB);
+    }
   }
-  const size_t rows = ngroups * g.nwin, ngw = 2 * rows;
+  const size_t rows = ngroups * g.nwin, ngw = (size_t)nsets * rows;
   hipLaunchKernelGGL(k_msm_segsum28<C>, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs,
                      ws.runs);
   if (g.nseg > 1)
@@ -966,7 +974,7 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     hipLaunchKernelGGL(k_msm_tree28<C>, dim3(nblk(ngw * half, 256)), dim3(256), 0, st, ws.segs, ngw, g.nseg, width, half);
     width = half;
   }
-  hipLaunchKernelGGL(k_msm_windows28<C>, dim3(nblk(2 * ngroups, 64)), dim3(64), 0, st, ws.segs, g, 2 * ngroups, ws.out2);
+  hipLaunchKernelGGL(k_msm_windows28<C>, dim3(nblk(nsets * ngroups, 64)), dim3(64), 0, st, ws.segs, g, nsets * ngroups, ws.out2);
   return hipGetLastError();
 }
 
@@ -1165,6 +1173,19 @@ hipError_t launch_group_sums28(int sig_g2, const uint32_t* entries, size_t m, si
   if (!m) return hipSuccess;
   return sig_g2 ? group_sums28<c28_g2>(entries, m, gsize, R, n, tmpA, tmpB, outA, outB, st)
                 : group_sums28<c28_g1>(entries, m, gsize, R, n, tmpA, tmpB, outA, outB, st);
+}
+
+// one point set of 28-bit points (launch_msm_prep28): entry e is point pidx[e] (+ its endomorphism images at
+// g.half_stride steps) with scalar scal[sidx ? sidx[e] : pidx[e]] in group grp ? grp[e] : e / g.gsize; out: ngroups
+// 12 x 32-bit Jacobian sums (the tbls Recover's VerifyPartial batch: all partials' sigmas, the hash points per signer)
+hipError_t launch_msm28_set(int sig_g2, const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp,
+                            size_t m, size_t ngroups, const uint4* scal, const uint32_t* P, msm_ws& ws, uint32_t* out,
+                            hipStream_t st) {
+  hipError_t e = launch_msm_sort(g, pidx, sidx, grp, m, ngroups, scal, ws, st);
+  if (e != hipSuccess) return e;
+  e = sig_g2 ? msm28<c28_g2>(g, ngroups, P, nullptr, ws, st, nullptr, 1) : msm28<c28_g1>(g, ngroups, P, nullptr, ws, st, nullptr, 1);
+  if (e != hipSuccess) return e;
+  return hipMemcpyAsync(out, ws.out2, ngroups * (sig_g2 ? 72 : 36) * 4, hipMemcpyDeviceToDevice, st);
 }
 
 // bisection: the entries of the failing groups, in order, on the device (groups are runs of gsize consecutive entries,

@@ -303,29 +303,39 @@ __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restric
   uint32_t* o = tbl + (size_t)TBL_WORDS * e;
 #pragma unroll
   for (int w = 0; w < A28_WORDS; w += 4) *(uint4*)(o + w) = *(const uint4*)(p + w);
-  const j228 two = j228_dbl(j228{px, py, f2_one(), false});
-  j228 m[3];
-  m[0] = j228_madd<true>(two, px, py);  // 3P
-  m[1] = j228_add<true>(m[0], two);     // 5P
-  m[2] = j228_add<true>(m[1], two);     // 7P
-  const f228 z01 = f2_red(f2_mul(m[0].z, m[1].z));
-  const f228 z012 = f2_red(f2_mul(z01, m[2].z));
-  f228 inv = f2_from_fp2(fp2_inv_vt(f2_to_fp2(z012)));  // 1 / (z0 z1 z2)
+  // 3P, 5P, 7P: X, Y parked in their table slots until the inversion, only the three Z's stay in registers
+  f228 z[3];
+  {
+    const j228 two = j228_dbl(j228{px, py, f2_one(), false});
+    j228 m = j228_madd<true>(two, px, py);  // 3P
+#pragma unroll 1
+    for (int k = 0; k < 3; k++) {
+      if (k) m = j228_add<true>(m, two);  // 5P, 7P
+      uint32_t* sl = o + A28_WORDS * (k + 1);
+      st_f28w(sl, m.x.c0);
+      st_f28w(sl + 16, m.x.c1);
+      st_f28w(sl + 32, m.y.c0);
+      st_f28w(sl + 48, m.y.c1);
+      z[k] = m.z;
+    }
+  }
+  const f228 z01 = f2_red(f2_mul(z[0], z[1]));
+  f228 inv = f2_from_fp2(fp2_inv_vt(f2_to_fp2(f2_red(f2_mul(z01, z[2])))));  // 1 / (z0 z1 z2)
   f228 zi[3];
   zi[2] = f2_red(f2_mul(inv, z01));
-  inv = f2_red(f2_mul(inv, m[2].z));                      // 1 / (z0 z1)
-  zi[1] = f2_red(f2_mul(inv, m[0].z));
-  zi[0] = f2_red(f2_mul(inv, m[1].z));
+  inv = f2_red(f2_mul(inv, z[2]));  // 1 / (z0 z1)
+  zi[1] = f2_red(f2_mul(inv, z[0]));
+  zi[0] = f2_red(f2_mul(inv, z[1]));
 #pragma unroll 1
   for (int k = 0; k < 3; k++) {
+    uint32_t* sl = o + A28_WORDS * (k + 1);
     const f228 z2 = f2_red(f2_sqr<2>(zi[k]));
-    const f228 x = f2_red(f2_mul(m[k].x, z2));
-    const f228 y = f2_red(f2_mul(m[k].y, f2_red(f2_mul(z2, zi[k]))));
-    uint32_t* ok2 = o + A28_WORDS * (k + 1);
-    st_f28w(ok2, x.c0);
-    st_f28w(ok2 + 16, x.c1);
-    st_f28w(ok2 + 32, y.c0);
-    st_f28w(ok2 + 48, y.c1);
+    const f228 x = f2_red(f2_mul(f228{ld_f28w(sl), ld_f28w(sl + 16)}, z2));
+    const f228 y = f2_red(f2_mul(f228{ld_f28w(sl + 32), ld_f28w(sl + 48)}, f2_red(f2_mul(z2, zi[k]))));
+    st_f28w(sl, x.c0);
+    st_f28w(sl + 16, x.c1);
+    st_f28w(sl + 32, y.c0);
+    st_f28w(sl + 48, y.c1);
   }
 }
 hipError_t launch_wnaf_table_g2(const uint32_t* aff28, const uint8_t* ok, size_t n, uint32_t* tbl, hipStream_t st) {

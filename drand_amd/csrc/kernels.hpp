@@ -90,7 +90,11 @@ hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, si
 // per point, 2n points each; a hash point at infinity marks its round DEC_BAD); the workspace's bucket / partial /
 // segment arrays hold 48 / 96-word Jacobian points
 hipError_t launch_msm_prep28(int sig_g2, size_t n, uint8_t* status, const uint32_t* sig_aff, const uint32_t* q_pts,
-                             uint32_t* S, uint32_t* Q, hipStream_t st);
+                             uint32_t* S, uint32_t* Q, hipStream_t st, uint32_t sets = 3);
+// one point set (S of launch_msm_prep28) with point / scalar / group indices: ngroups 12 x 32-bit Jacobian sums into out
+hipError_t launch_msm28_set(int sig_g2, const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp,
+                            size_t m, size_t ngroups, const uint4* scal, const uint32_t* P, msm_ws& ws, uint32_t* out,
+                            hipStream_t st);
 hipError_t launch_msm28(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
                         const uint32_t* S, const uint32_t* Q, msm_ws& ws, uint32_t* outA, uint32_t* outB, hipStream_t st,
                         const uint8_t* skip, bool presorted);

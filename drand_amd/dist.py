@@ -240,8 +240,14 @@ def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, pa
     stream = torch.cuda.current_stream(partials.device) if partials.is_cuda else None
     # inputs still in production on the current stream are waited for; resident inputs (inputs_ready: the bench) are
     # not, since the current stream also carries the earlier batches' verdict packing, queued behind other batches'
-    # saturating kernels (r04c: ordering on it cost the 131k-round node shape ~20%)
-    sp = ctypes.c_void_p(stream.cuda_stream) if stream is not None and not inputs_ready else None
+    # saturating kernels (r04c: ordering on it cost the 131k-round node shape ~20%). torch's default stream is the
+    # NULL stream, whose handle the library reads as "no stream": its work is waited for on the host instead.
+    sp = None
+    if stream is not None and not inputs_ready:
+        if stream.cuda_stream:
+            sp = ctypes.c_void_p(stream.cuda_stream)
+        else:
+            stream.synchronize()
     b = ctypes.c_void_p()
     rc = lib.dh_batch_begin(scheme.id, pk, len(pk), ptr(d_rounds), ptr(d_sigs), scheme.sig_len, ptr(d_prevs),
                             prev_stride, ptr(d_prev_lens), n, ptr(d_verdict), ptr(d_rand), rank_seed(seed, rank), sp,

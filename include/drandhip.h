@@ -171,7 +171,8 @@ int dh_verify_partials_batch(int scheme, const uint8_t* commits, int t, int n_no
  * record, the all-gather and the check follow each other in stream order, with no host wait and, for one rank, no
  * cross-stream wait. dh_batch_begin returns as soon as the batch is queued; with hip_stream (a hipStream_t) non-NULL
  * it orders the batch after hip_stream's work (inputs still in production there), with NULL the inputs must be
- * complete. A host caller that wants the record itself waits for dh_batch_stream(b).
+ * complete (NULL means "no stream": work on the legacy NULL / default stream must be synchronised by the caller).
+ * A host caller that wants the record itself waits for dh_batch_stream(b).
  * dh_batch_check orders the check after hip_stream's work when hip_stream is another stream (the gathered records
  * produced there); NULL or dh_batch_stream(b) adds no wait. The only host wait of a batch is in dh_batch_finish.
  *

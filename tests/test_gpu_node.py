@@ -130,8 +130,12 @@ def test_node_wide_check_all_schemes(dh, oracle, name, mode):
         parts = torch.zeros(len(shards) * pb, dtype=torch.uint8, device=dev)
         handles = []
         sl = s.sig_len
-        cur = torch.cuda.current_stream(dev)
+        # an explicit stream: torch's default stream is the NULL stream, which the library reads as "no stream"
+        cur = torch.cuda.Stream(device=dev)
+        cur.wait_stream(torch.cuda.current_stream(dev))  # the inputs above
         sp = ctypes.c_void_p(cur.cuda_stream) if mode == "device" else None
+        if mode == "host":
+            torch.cuda.synchronize()
         for k, (lo, hi) in enumerate(shards):
             b = ctypes.c_void_p()
             rc = lib.dh_batch_begin(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr() + 8 * lo),
@@ -148,7 +152,8 @@ def test_node_wide_check_all_schemes(dh, oracle, name, mode):
             # three, and each check is ordered after the current stream's work
             for b in handles:
                 cur.wait_stream(torch.cuda.ExternalStream(lib.dh_batch_stream(b), device=dev))
-            snap = parts.clone()
+            with torch.cuda.stream(cur):
+                snap = parts.clone()
             results, stats = [], []
             for b in handles:
                 assert lib.dh_batch_check(b, ctypes.c_void_p(parts.data_ptr()), len(shards), sp) == 0, _lib.last_error()
@@ -217,7 +222,9 @@ def test_node_batch_abandoned(dh):
     pb = lib.dh_partial_bytes(s.id)
     parts = torch.zeros(2 * pb, dtype=torch.uint8, device=dev)
     parts[2 * pb - 16] = 1  # the second rank's record: began nothing, status 1
-    sp = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    cur = torch.cuda.Stream(device=dev)  # explicit: the default stream is the NULL stream ("no stream" to the library)
+    cur.wait_stream(torch.cuda.current_stream(dev))
+    sp = ctypes.c_void_p(cur.cuda_stream)
     b = ctypes.c_void_p()
     assert lib.dh_batch_begin(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr()), ctypes.c_void_p(d_s.data_ptr()), 48,
                               None, 0, None, n, ctypes.c_void_p(d_v.data_ptr()), None, 3, sp, ctypes.byref(b),
