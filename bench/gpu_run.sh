@@ -11,6 +11,7 @@
 #   rocprof[:<args>]       rocprofv3 --kernel-trace --stats of python3 bench.py <args> -> gpurun_out/prof_<tag>_<i>/
 #   pmc:<counters>[@<args>] one rocprofv3 --pmc pass of bench.py <args> -> gpurun_out/pmc_<tag>_<i>/
 #   py:<script args>       python <script args>              -> gpurun_out/py_<tag>_<i>.log
+#   env:<NAME>=<value>     export a variable for the steps after it (env:NAME= clears it)
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
@@ -56,6 +57,8 @@ for step in "$@"; do
     py)
       timeout -k 10 600 python $arg > "$O/py_${T}_$i.log" 2>&1
       tail -5 "$O/py_${T}_$i.log" ;;
+    env)
+      export "$arg" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -114,7 +114,7 @@ struct worker {
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
-      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_aff28, r_tbl, r_rstat;
+      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_zs, r_tbl, r_rstat;
   std::vector<uint8_t> h_verdict;
   // decoded group key cache: the same key is used for every batch of a chain
   uint8_t cached_key[96];
@@ -130,7 +130,7 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_aff28, &r_tbl, &r_rstat, &node_sum, &node_res, &tree_r,
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_zs, &r_tbl, &r_rstat, &node_sum, &node_res, &tree_r,
                    &tree_a, &tree_b};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
@@ -628,11 +628,32 @@ static size_t next_group_size(size_t gsize, size_t ngroups, size_t nfail, size_t
 }
 
 // Bisection from scaled points (launch_scale28 once per batch, then launch_group_sums28 per level) instead of an MSM
-// per level; DRANDHIP_BISECT_TREE=0 keeps the per-level MSMs (the r03 path, for comparison)
+// per level: OFF by default (DRANDHIP_BISECT_TREE=1 selects it). Measured on the chained 4M replay at 0.1% Cfg5
+// corruption (gpurun_out r04d): 3.45 M beacons/s against 5.34 with the per-level MSMs — k_scale28 took ~430 ms per
+// 1M-round window, because every lane scales its own random scalar: at each bit some lane of the wave has a nonzero
+// NAF digit in every part, so the wave runs every part's addition at nearly every position (~128 additions per point
+// instead of ~41), at one wave per SIMD. The per-level Pippenger keeps the wave uniform.
+static bool prep_sync() {
+  static const bool v = [] {
+    const char* e = getenv("DRANDHIP_PREP_SYNC");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// DRANDHIP_SKIP_LEVEL0=0 keeps level 0 on dense-fault workers (comparison runs)
+static bool skip_level0() {
+  static const bool v = [] {
+    const char* e = getenv("DRANDHIP_SKIP_LEVEL0");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 static bool tree_bisection() {
   static const bool v = [] {
     const char* e = getenv("DRANDHIP_BISECT_TREE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return v;
 }
@@ -706,6 +727,11 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   const bool tree_ok = msm28 && tree_bisection();
   const bool tree_first = tree_ok && mode <= VM_BEGIN && w->fault_density > 1.0 / 2000 && n > 4096;
   bool tree = tree_first, scaled = false;
+  // A local batch on a worker whose last bisection saw dense faults skips level 0: its one group is expected to fail,
+  // so the batch starts at the dense ladder's 256-round groups (their check also answers "is the batch clean": a
+  // batch whose groups all pass clears the hint). Saves the level-0 MSM and pairing check per dense window.
+  // (with a fixed ladder, DRANDHIP_BISECT, its first size)
+  const bool skip0 = !tree_first && mode == VM_FULL && w->fault_density > 1.0 / 2000 && n > 4096 && skip_level0();
   dh::msm_geom g0{};
   dh::msm_ws ws0{};
   if (mode <= VM_BEGIN) {
@@ -727,7 +753,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     // while the per-round kernels decode and hash (its ~1 ms of small kernels left the one-call latency path).
     // Every round then carries a scalar; the bucket passes skip rounds whose status is not DEC_OK. A worker whose
     // last bisection saw dense faults takes level 0 from the scaled points instead (no sort).
-    presorted = w->tail && st == w->stream && !tree_first;
+    presorted = w->tail && st == w->stream && !tree_first && !skip0;
     if (presorted) {
       hipStream_t ts = w->tail;
       HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, ts));
@@ -770,8 +796,12 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
       HIP_TRY(hipEventRecord(gate->done, st));
       gate->recorded();
     }
-    // no host wait here: the tail below is queued behind the per-round kernels (r03 synchronised the stream at this
-    // point, a host round trip per batch before the MSM could even be queued)
+    // The node batch (VM_BEGIN) queues its tail behind the per-round kernels with no host wait. A local batch
+    // (VM_FULL) waits here first, as r03 did: its tail stream then carries no event wait while the per-round kernels
+    // run, and with 8 batches in flight (16+ streams on 16 hardware queues) a queue blocked on such a wait holds up
+    // the streams that share it (quicknet 1M: 25.5-25.9 M/s without this wait, 26.4-26.5 with it; DRANDHIP_PREP_SYNC=0
+    // drops it for comparison).
+    if (mode == VM_FULL && w->tail && st == w->stream && prep_sync()) HIP_TRY(hipStreamSynchronize(st));
     if (!presorted) HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
   }
   // the tail (MSM, checks, bisection) runs on the worker's high-priority stream, after the per-round kernels
@@ -793,8 +823,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
                                            "k_group_check_bisect3", "k_group_check_bisect4", "k_group_check_bisect5",
                                            "k_group_check_bisect6", "k_group_check_bisect7+"};
   const std::vector<size_t>& fixed = fixed_ladder();
-  size_t gsize = n;
-  int level = 0;
+  size_t gsize = skip0 ? (fixed.empty() ? 256 : fixed[0]) : n;
+  int level = skip0 ? 1 : 0;
   if (mode == VM_BEGIN && n < 2) {
     // a one-round batch has no level-0 group: it contributes the identity (Z = 0) to the node-wide sums, and
     // dh_batch_finish gives the round its own leaf check whatever the node check says
@@ -1082,17 +1112,17 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   }));
   // 13. interpolation on the device
   if (g2) {  // the partials' points in the 28-bit form, and their width-4 NAF tables, once per valid partial
-    HIP_TRY(w->r_aff28.ensure(np * 64 * 4 + 256));
+    HIP_TRY(w->r_zs.ensure(dh::wnaf_table_scratch_bytes(np) + 256));
     HIP_TRY(w->r_tbl.ensure(np * 256 * 4 + 1024));
-    HIP_TRY(dh::launch_aff28_g2(w->r_paff.as<uint32_t>(), np, w->r_aff28.as<uint32_t>(), st));
     HIP_TRY(T.run("k_wnaf_table", [&] {
-      return dh::launch_wnaf_table_g2(w->r_aff28.as<uint32_t>(), w->r_ok.as<uint8_t>(), np, w->r_tbl.as<uint32_t>(), st);
+      return dh::launch_wnaf_table_g2(w->r_paff.as<uint32_t>(), w->r_ok.as<uint8_t>(), np, w->r_tbl.as<uint32_t>(),
+                                      w->r_zs.as<uint32_t>(), st);
     }));
   }
   HIP_TRY(T.run("k_lagrange", [&] {
     return dh::launch_lagrange(g2, w->r_sel.as<uint32_t>(), w->r_lam.as<uint32_t>(), nullptr, w->r_rok.as<uint8_t>(), t,
-                               n_rounds, w->r_paff.as<uint32_t>(), g2 ? w->r_aff28.as<uint32_t>() : nullptr,
-                               g2 ? w->r_tbl.as<uint32_t>() : nullptr, w->r_sig.as<uint32_t>(), st);
+                               n_rounds, w->r_paff.as<uint32_t>(), g2 ? w->r_tbl.as<uint32_t>() : nullptr,
+                               w->r_sig.as<uint32_t>(), st);
   }));
   std::vector<uint8_t> rok(n_rounds, 0);
   HIP_TRY(hipMemcpyAsync(rok.data(), w->r_rok.p, n_rounds, hipMemcpyDeviceToHost, st));

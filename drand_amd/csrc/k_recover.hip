@@ -251,8 +251,8 @@ constexpr int LG_LANES = 4, LG_MAXK = 9;  // terms per lane and pass (t <= 36: o
 // P, 3P, 5P, 7P (1/5 of the positions take an addition instead of 1/3), with the MSM's fast mixed additions (no
 // exceptional-case tests); a chain that met an exceptional case ends with Z = 0 mod p and runs again with the exact
 // formulas. G1 keeps the 32-bit Straus chain over the NAF masks.
-// the partial signatures' affine points in the 28-bit form, converted once per partial (k_aff28_g2) instead of at each
-// of the ~85 additions per term that read them: x.c0, x.c1, y.c0, y.c1, 16 words each (14 limbs + 2 pad)
+// a point coordinate pair in the 28-bit form as the tables hold it, converted once per partial (k_wnaf_table_g2)
+// instead of at each of the additions that read it: x.c0, x.c1, y.c0, y.c1, 16 words each (14 limbs + 2 pad)
 constexpr int A28_WORDS = 64;
 DH_DEV f28 ld_f28w(const uint32_t* p) {
   f28 a;
@@ -273,76 +273,90 @@ DH_DEV void st_f28w(uint32_t* p, const f28& a) {
   for (int i = 0; i < 4; i++)
     q[i] = make_uint4(a.l[4 * i], a.l[4 * i + 1], 4 * i + 2 < 14 ? a.l[4 * i + 2] : 0u, 4 * i + 3 < 14 ? a.l[4 * i + 3] : 0u);
 }
-__global__ __launch_bounds__(256) void k_aff28_g2(const uint32_t* __restrict__ pts, size_t n, uint32_t* __restrict__ out) {
-  const size_t i = gtid();
-  if (i >= n) return;
-  const aff<fp2> a = ld_aff_aos<fp2>(pts, i);
-  uint32_t* o = out + (size_t)A28_WORDS * i;
-  st_f28w(o, f28_from_fp(a.x.c0));
-  st_f28w(o + 16, f28_from_fp(a.x.c1));
-  st_f28w(o + 32, f28_from_fp(a.y.c0));
-  st_f28w(o + 48, f28_from_fp(a.y.c1));
+// G2 width-4 NAF table per valid partial: P, 3P, 5P, 7P affine in the 28-bit form (WT x 64 words). The Jacobian Z's
+// of 3P, 5P, 7P are inverted with Montgomery's trick over TB_K partials per lane (one variable-time Fp2 inversion per
+// lane instead of per partial: r04d spent 30.6 ms on 3.3M tables with one inversion each); the lane parks each
+// partial's three Z's and the running product before it in zs (128 words per partial) and walks back after the
+// inversion. The partials reaching k_lagrange decoded to subgroup points, so 2P, 3P, 5P, 7P are finite and distinct
+// from the points added to them: the exact formulas only guard the table of a partial that is never selected.
+constexpr int WT = 4, TBL_WORDS = WT * A28_WORDS, TB_K = 8, ZS_WORDS = 128;
+DH_DEV void st_f228w(uint32_t* p, const f228& a) {
+  st_f28w(p, a.c0);
+  st_f28w(p + 16, a.c1);
 }
-hipError_t launch_aff28_g2(const uint32_t* pts, size_t n, uint32_t* out, hipStream_t st) {
-  if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_aff28_g2, dim3(nblk(n, 256)), dim3(256), 0, st, pts, n, out);
-  return hipGetLastError();
-}
-
-// G2 width-4 NAF table per valid partial: P, 3P, 5P, 7P affine in the 28-bit form (WT x 64 words), from one
-// variable-time Fp2 inversion of the three Jacobian Z's (Montgomery's trick; public values). The partials reaching
-// k_lagrange decoded to subgroup points, so 2P, 3P, 5P, 7P are finite and distinct from the points added to them: the
-// exact formulas only guard the table of a partial that is never selected.
-constexpr int WT = 4, TBL_WORDS = WT * A28_WORDS;
-__global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restrict__ aff28, const uint8_t* __restrict__ ok,
-                                                       size_t n, uint32_t* __restrict__ tbl) {
-  const size_t e = gtid();
-  if (e >= n || !ok[e]) return;
-  const uint32_t* p = aff28 + (size_t)A28_WORDS * e;
-  const f228 px{ld_f28w(p), ld_f28w(p + 16)}, py{ld_f28w(p + 32), ld_f28w(p + 48)};
-  uint32_t* o = tbl + (size_t)TBL_WORDS * e;
-#pragma unroll
-  for (int w = 0; w < A28_WORDS; w += 4) *(uint4*)(o + w) = *(const uint4*)(p + w);
-  // 3P, 5P, 7P: X, Y parked in their table slots until the inversion, only the three Z's stay in registers
-  f228 z[3];
-  {
+DH_DEV f228 ld_f228w(const uint32_t* p) { return f228{ld_f28w(p), ld_f28w(p + 16)}; }
+__global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restrict__ paff, const uint8_t* __restrict__ ok,
+                                                       size_t n, uint32_t* __restrict__ tbl, uint32_t* __restrict__ zs) {
+  const size_t nth = (n + TB_K - 1) / TB_K;
+  const size_t t = gtid();
+  if (t >= nth) return;
+  f228 pre = f2_one();
+  uint32_t valid = 0;  // bit k: the lane's k-th partial is valid
+#pragma unroll 1
+  for (int k = 0; k < TB_K; k++) {
+    const size_t e = t + (size_t)k * nth;  // lanes of a wave take consecutive partials
+    if (e >= n || !ok[e]) continue;
+    const aff<fp2> a = ld_aff_aos<fp2>(paff, e);
+    const f228 px{f28_from_fp(a.x.c0), f28_from_fp(a.x.c1)}, py{f28_from_fp(a.y.c0), f28_from_fp(a.y.c1)};
+    uint32_t* o = tbl + (size_t)TBL_WORDS * e;
+    uint32_t* z = zs + (size_t)ZS_WORDS * e;
+    st_f228w(o, px);
+    st_f228w(o + 32, py);
+    // 3P, 5P, 7P: X, Y parked in their table slots, Z's in zs, until the inversion
     const j228 two = j228_dbl(j228{px, py, f2_one(), false});
     j228 m = j228_madd<true>(two, px, py);  // 3P
+    f228 zp = f2_one();
 #pragma unroll 1
-    for (int k = 0; k < 3; k++) {
-      if (k) m = j228_add<true>(m, two);  // 5P, 7P
-      uint32_t* sl = o + A28_WORDS * (k + 1);
-      st_f28w(sl, m.x.c0);
-      st_f28w(sl + 16, m.x.c1);
-      st_f28w(sl + 32, m.y.c0);
-      st_f28w(sl + 48, m.y.c1);
-      z[k] = m.z;
+    for (int j = 0; j < 3; j++) {
+      if (j) m = j228_add<true>(m, two);  // 5P, 7P
+      uint32_t* sl = o + A28_WORDS * (j + 1);
+      st_f228w(sl, m.x);
+      st_f228w(sl + 32, m.y);
+      st_f228w(z + 32 * j, m.z);
+      zp = j ? f2_red(f2_mul(zp, m.z)) : m.z;
+    }
+    if (valid) st_f228w(z + 96, pre);  // the product of the lane's earlier Z's
+    pre = valid ? f2_red(f2_mul(pre, zp)) : zp;
+    valid |= 1u << k;
+  }
+  if (!valid) return;
+  f228 inv = f2_from_fp2(fp2_inv_vt(f2_to_fp2(pre)));  // 1 / (product of every Z of the lane)
+#pragma unroll 1
+  for (int k = TB_K - 1; k >= 0; k--) {
+    if (!(valid >> k & 1)) continue;
+    const size_t e = t + (size_t)k * nth;
+    const uint32_t* z = zs + (size_t)ZS_WORDS * e;
+    const f228 z0 = ld_f228w(z), z1 = ld_f228w(z + 32), z2 = ld_f228w(z + 64);
+    const f228 z01 = f2_red(f2_mul(z0, z1));
+    // this partial's 1 / (z0 z1 z2): inv times the product of the Z's before it (the lane's first: inv itself);
+    // inv then becomes 1 / that product
+    f228 ip = inv;
+    if (valid & ((1u << k) - 1)) {
+      ip = f2_red(f2_mul(inv, ld_f228w(z + 96)));
+      inv = f2_red(f2_mul(inv, f2_red(f2_mul(z01, z2))));
+    }
+    f228 zi[3];
+    zi[2] = f2_red(f2_mul(ip, z01));
+    const f228 i01 = f2_red(f2_mul(ip, z2));  // 1 / (z0 z1)
+    zi[1] = f2_red(f2_mul(i01, z0));
+    zi[0] = f2_red(f2_mul(i01, z1));
+    uint32_t* o = tbl + (size_t)TBL_WORDS * e;
+#pragma unroll 1
+    for (int j = 0; j < 3; j++) {
+      uint32_t* sl = o + A28_WORDS * (j + 1);
+      const f228 z2j = f2_red(f2_sqr<2>(zi[j]));
+      st_f228w(sl, f2_red(f2_mul(ld_f228w(sl), z2j)));
+      st_f228w(sl + 32, f2_red(f2_mul(ld_f228w(sl + 32), f2_red(f2_mul(z2j, zi[j])))));
     }
   }
-  const f228 z01 = f2_red(f2_mul(z[0], z[1]));
-  f228 inv = f2_from_fp2(fp2_inv_vt(f2_to_fp2(f2_red(f2_mul(z01, z[2])))));  // 1 / (z0 z1 z2)
-  f228 zi[3];
-  zi[2] = f2_red(f2_mul(inv, z01));
-  inv = f2_red(f2_mul(inv, z[2]));  // 1 / (z0 z1)
-  zi[1] = f2_red(f2_mul(inv, z[0]));
-  zi[0] = f2_red(f2_mul(inv, z[1]));
-#pragma unroll 1
-  for (int k = 0; k < 3; k++) {
-    uint32_t* sl = o + A28_WORDS * (k + 1);
-    const f228 z2 = f2_red(f2_sqr<2>(zi[k]));
-    const f228 x = f2_red(f2_mul(f228{ld_f28w(sl), ld_f28w(sl + 16)}, z2));
-    const f228 y = f2_red(f2_mul(f228{ld_f28w(sl + 32), ld_f28w(sl + 48)}, f2_red(f2_mul(z2, zi[k]))));
-    st_f28w(sl, x.c0);
-    st_f28w(sl + 16, x.c1);
-    st_f28w(sl + 32, y.c0);
-    st_f28w(sl + 48, y.c1);
-  }
 }
-hipError_t launch_wnaf_table_g2(const uint32_t* aff28, const uint8_t* ok, size_t n, uint32_t* tbl, hipStream_t st) {
+hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, uint32_t* tbl, uint32_t* zs,
+                                hipStream_t st) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_wnaf_table_g2, dim3(nblk(n, 256)), dim3(256), 0, st, aff28, ok, n, tbl);
+  hipLaunchKernelGGL(k_wnaf_table_g2, dim3(nblk((n + TB_K - 1) / TB_K, 256)), dim3(256), 0, st, paff, ok, n, tbl, zs);
   return hipGetLastError();
 }
+size_t wnaf_table_scratch_bytes(size_t n) { return n * ZS_WORDS * 4; }
 
 // the width-4 NAF Straus chain of one lane's terms over their tables (nibble words of the current 8 positions in nw)
 template <bool EXACT>
@@ -373,7 +387,7 @@ template <class F>
 __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __restrict__ sel, const uint32_t* __restrict__ lam,
                                                             const uint32_t* __restrict__ lam_set, const uint8_t* __restrict__ ok,
                                                             int t, size_t n_rounds, const uint32_t* __restrict__ sig_aff,
-                                                            const uint32_t* __restrict__ aff28, const uint32_t* __restrict__ tbl,
+                                                            const uint32_t* __restrict__ tbl,
                                                             uint32_t* __restrict__ out) {
   constexpr int JW = sizeof(F) / 4 * 3;
   __shared__ uint32_t part[(LG_LANES - 1) * 64 * JW];  // the partial sums of waves 1 .. LG_LANES - 1
@@ -530,15 +544,15 @@ hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const 
 }
 
 hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
-                           int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* aff28, const uint32_t* tbl,
-                           uint32_t* out, hipStream_t st) {
+                           int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, uint32_t* out,
+                           hipStream_t st) {
   if (!n_rounds) return hipSuccess;
   if (sig_g2)
     hipLaunchKernelGGL(k_lagrange<fp2>, dim3(nblk(n_rounds, 64)), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t,
-                       n_rounds, sig_aff, aff28, tbl, out);
+                       n_rounds, sig_aff, tbl, out);
   else
     hipLaunchKernelGGL(k_lagrange<fp>, dim3(nblk(n_rounds, 64)), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t,
-                       n_rounds, sig_aff, aff28, tbl, out);
+                       n_rounds, sig_aff, tbl, out);
   return hipGetLastError();
 }
 

@@ -166,13 +166,14 @@ hipError_t launch_ok_from_status(const uint8_t* status, size_t np, uint8_t* ok, 
 // per round: Recover's selection + Lagrange coefficients (sel/key: t words, den: 8t words, lam: 48t words per round)
 hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const uint32_t* share_idx, int t, size_t n_rounds,
                                   uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint8_t* rok, hipStream_t st);
-// aff28 (G2): the partials' points in the 28-bit form of launch_aff28_g2 (64 words each); unused for G1
-hipError_t launch_aff28_g2(const uint32_t* aff, size_t n, uint32_t* out, hipStream_t st);
-// tbl (G2): per valid partial (ok) P, 3P, 5P, 7P affine 28-bit (launch_wnaf_table_g2, 256 words each)
-hipError_t launch_wnaf_table_g2(const uint32_t* aff28, const uint8_t* ok, size_t n, uint32_t* tbl, hipStream_t st);
+// tbl (G2): per valid partial (ok) P, 3P, 5P, 7P affine 28-bit (256 words each) from the partials' affine points
+// (12 x 32-bit AOS); zs: wnaf_table_scratch_bytes(n) of scratch (the batched inversion's Z's); unused for G1
+hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, uint32_t* tbl, uint32_t* zs,
+                                hipStream_t st);
+size_t wnaf_table_scratch_bytes(size_t n);
 hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
-                           int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* aff28, const uint32_t* tbl,
-                           uint32_t* out, hipStream_t st);
+                           int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, uint32_t* out,
+                           hipStream_t st);
 hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, hipStream_t st);
 hipError_t launch_recover_pairs(int sig_g2, const uint32_t* shares, const uint32_t* B, const uint32_t* A, int n_nodes,
                                 uint32_t* P, uint32_t* Q, hipStream_t st);

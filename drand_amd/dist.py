@@ -120,8 +120,9 @@ def pack_bits(verdict):
     n = verdict.numel()
     pad = (-n) % 8
     v = torch.nn.functional.pad(verdict.to(torch.uint8), (0, pad)).view(-1, 8).to(torch.int32)
-    w = torch.tensor([128, 64, 32, 16, 8, 4, 2, 1], dtype=torch.int32, device=verdict.device)
-    return (v * w).sum(dim=1).to(torch.uint8)
+    # bit weights made on the device (arange): a host-built tensor is a pageable copy that waits for the queue
+    sh = torch.arange(7, -1, -1, dtype=torch.int32, device=verdict.device)
+    return (v << sh).sum(dim=1).to(torch.uint8)
 
 
 class NodeFailure(RuntimeError):

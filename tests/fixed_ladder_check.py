@@ -32,7 +32,7 @@ for k, i in enumerate(bad):
 v, _ = s.verify_beacons(pk, rounds, sigs, seed=21)
 out = {"rejected": np.flatnonzero(~v).tolist(), "expected": bad.tolist()}
 # the same batch again: the worker's first bisection saw dense faults (0.5%), so with the scaled-point bisection
-# this call takes level 0 from the scaled points too (no level-0 MSM)
+# (DRANDHIP_BISECT_TREE=1) this call takes level 0 from the scaled points too (no level-0 MSM)
 v2, _ = s.verify_beacons(pk, rounds, sigs, seed=22)
 out["rejected_again"] = np.flatnonzero(~v2).tolist()
 

@@ -151,6 +151,13 @@ def test_dense_corruption_every_window_geometry(dh):
     assert np.flatnonzero(~v).tolist() == bad.tolist()
     for i in [0, int(bad[0]), n - 1]:
         assert rand[i].tobytes() == hashlib.sha256(sigs2[i].tobytes()).digest()
+    # again: the worker's last bisection saw dense faults, so this batch skips level 0 and starts at 256-round
+    # groups (drandhip.cpp skip0); then a clean batch on the dense hint, whose 256-groups all pass
+    v, _ = s.verify_beacons(pk, rounds, sigs2, seed=13)
+    assert np.flatnonzero(~v).tolist() == bad.tolist()
+    s.verify_beacons(pk, rounds, sigs2, seed=14)
+    v, _ = s.verify_beacons(pk, rounds, sigs, seed=15)
+    assert v.all()
     m = 300
     sigs3 = np.ascontiguousarray(np.roll(sigs[:m], 1, axis=0))  # every signature belongs to another round
     v3, _ = s.verify_beacons(pk, rounds[:m], sigs3, seed=12)
@@ -336,8 +343,8 @@ def test_fixed_bisection_ladder(dh, ladder, tree):
     """The bisection is exact whatever the group sizes: a fixed ladder (DRANDHIP_BISECT, the r01 sizes with the
     c = 10 window geometry, and a single level of 64 before leaves) rejects exactly the corrupted rounds, as the
     default expected-cost ladder does in the tests above — with the level sums taken from per-round scaled points
-    (tree "1", the default; the second quicknet call, after a dense first one, also takes level 0 from them) and from a
-    grouped MSM per level (tree "0"). The G2 statistics pin the sums themselves: exactly one failing group per level."""
+    (tree "1", opt-in; the second quicknet call, after a dense first one, also takes level 0 from them) and from a
+    grouped MSM per level (tree "0", the default). The G2 statistics pin the sums themselves: exactly one failing group per level."""
     import subprocess
     import sys
     env = dict(os.environ, DRANDHIP_BISECT=ladder, DRANDHIP_BISECT_TREE=tree)
