@@ -114,7 +114,7 @@ struct worker {
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
-      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_zs, r_tbl, r_rstat;
+      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_zs, r_tbl, r_rstat, r_ltmp;
   std::vector<uint8_t> h_verdict;
   // decoded group key cache: the same key is used for every batch of a chain
   uint8_t cached_key[96];
@@ -130,7 +130,7 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_zs, &r_tbl, &r_rstat, &node_sum, &node_res, &tree_r,
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_zs, &r_tbl, &r_rstat, &r_ltmp, &node_sum, &node_res, &tree_r,
                    &tree_a, &tree_b};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
@@ -976,12 +976,26 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   HIP_TRY(w->r_pidx.ensure(np * 4 + 4));
   HIP_TRY(w->r_pstatus.ensure(np + 4));
   HIP_TRY(w->r_paff.ensure(np * aw * 4 + 16));
-  HIP_TRY(hipMemcpyAsync(w->r_raw.p, partials + (size_t)base * (2 + sl), np * (2 + sl), hipMemcpyHostToDevice, st));
-  HIP_TRY(dh::launch_repack_partials(w->r_raw.as<uint8_t>(), np, sl, w->r_psigs.as<uint8_t>(), w->r_pidx.as<uint32_t>(), st));
-  HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>(partials)" : "k_prep_sig<fp>(partials)", [&] {
-    return dh::launch_prep(g2, w->r_psigs.as<uint8_t>(), sl, np, w->r_pstatus.as<uint8_t>(), w->r_paff.as<uint32_t>(),
-                           nullptr, st);
-  }));
+  // The partial records (98 B each for G2: 323 MB at 3.3M partials) come from pageable host memory. They cross in
+  // chunks on the worker's tail stream, each chunk's repack + decode queued behind its copy on st, so the copy of
+  // chunk c + 1 overlaps the decoding of chunk c instead of preceding all of it.
+  const size_t pchunk = (w->tail && st == w->stream && np > ((size_t)1 << 19)) ? ((size_t)1 << 19) : np;
+  for (size_t c0 = 0; c0 < np; c0 += pchunk) {
+    const size_t cn = std::min(pchunk, np - c0);
+    hipStream_t cs = pchunk < np ? w->tail : st;
+    HIP_TRY(hipMemcpyAsync(w->r_raw.as<uint8_t>() + c0 * (2 + sl), partials + (size_t)(base + c0) * (2 + sl), cn * (2 + sl),
+                           hipMemcpyHostToDevice, cs));
+    if (cs != st) {
+      HIP_TRY(hipEventRecord(w->handoff, cs));
+      HIP_TRY(hipStreamWaitEvent(st, w->handoff, 0));
+    }
+    HIP_TRY(dh::launch_repack_partials(w->r_raw.as<uint8_t>() + c0 * (2 + sl), cn, sl, w->r_psigs.as<uint8_t>() + c0 * sl,
+                                       w->r_pidx.as<uint32_t>() + c0, st));
+    HIP_TRY(T.run(g2 ? "k_prep_sig<fp2>(partials)" : "k_prep_sig<fp>(partials)", [&] {
+      return dh::launch_prep(g2, w->r_psigs.as<uint8_t>() + c0 * sl, sl, cn, w->r_pstatus.as<uint8_t>() + c0,
+                             w->r_paff.as<uint32_t>() + c0 * aw, nullptr, st);
+    }));
+  }
   // 5. hash points of the round messages
   HIP_TRY(w->r_msgs.ensure(n_rounds * 32));
   HIP_TRY(w->r_q.ensure(n_rounds * jw * 4));
@@ -1119,10 +1133,11 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
                                       w->r_zs.as<uint32_t>(), st);
     }));
   }
+  HIP_TRY(w->r_ltmp.ensure(dh::lagrange_tmp_bytes(g2)));
   HIP_TRY(T.run("k_lagrange", [&] {
     return dh::launch_lagrange(g2, w->r_sel.as<uint32_t>(), w->r_lam.as<uint32_t>(), nullptr, w->r_rok.as<uint8_t>(), t,
                                n_rounds, w->r_paff.as<uint32_t>(), g2 ? w->r_tbl.as<uint32_t>() : nullptr,
-                               w->r_sig.as<uint32_t>(), st);
+                               w->r_sig.as<uint32_t>(), w->r_ltmp.as<uint32_t>(), st);
   }));
   std::vector<uint8_t> rok(n_rounds, 0);
   HIP_TRY(hipMemcpyAsync(rok.data(), w->r_rok.p, n_rounds, hipMemcpyDeviceToHost, st));

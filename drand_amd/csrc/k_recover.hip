@@ -360,13 +360,13 @@ size_t wnaf_table_scratch_bytes(size_t n) { return n * ZS_WORDS * 4; }
 
 // the width-4 NAF Straus chain of one lane's terms over their tables (nibble words of the current 8 positions in nw)
 template <bool EXACT>
-DH_DEV j228 lagrange_wnaf28(const uint32_t* __restrict__ L, int q, int c0, int nc, const uint32_t* __restrict__ tbl,
+DH_DEV j228 lagrange_wnaf28(const uint32_t* __restrict__ L, int q, int nl, int c0, int nc, const uint32_t* __restrict__ tbl,
                             const uint32_t* idx, uint32_t* nw) {
   j228 acc = j228_inf();
 #pragma unroll 1
   for (int b = 255; b >= 0; b--) {
     if ((b & 7) == 7)
-      for (int i = 0; i < nc; i++) nw[i] = L[(size_t)(q + LG_LANES * (c0 + i)) * LAM_WORDS + 16 + (b >> 3)];
+      for (int i = 0; i < nc; i++) nw[i] = L[(size_t)(q + nl * (c0 + i)) * LAM_WORDS + 16 + (b >> 3)];
     if (!acc.inf) acc = j228_dbl(acc);
 #pragma unroll 1
     for (int i = 0; i < nc; i++) {
@@ -383,35 +383,44 @@ DH_DEV j228 lagrange_wnaf28(const uint32_t* __restrict__ L, int q, int c0, int n
   return acc;
 }
 
+// Blocks [0, full) take every term of their 64 rounds (term lanes q = 0 .. LG_LANES - 1, written to out); the
+// remainder blocks, the last partial wave of workgroups over the chip, are split into S slices each (grid entries
+// full + r * S + s): slice s runs term lanes s * LG_LANES + q of NL = S * LG_LANES and writes its partial sum to
+// part_out[(j - 64 full) * S + s], summed into out by k_lagrange_sum. At 100k rounds the 1,563 blocks are 6 waves of
+// 256 CUs and 27 blocks whose full-length chains left the other CUs idle for the 7th (~12% of the kernel); sliced,
+// that wave's chains are ~1/3 as long.
 template <class F>
 __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __restrict__ sel, const uint32_t* __restrict__ lam,
                                                             const uint32_t* __restrict__ lam_set, const uint8_t* __restrict__ ok,
                                                             int t, size_t n_rounds, const uint32_t* __restrict__ sig_aff,
-                                                            const uint32_t* __restrict__ tbl,
-                                                            uint32_t* __restrict__ out) {
+                                                            const uint32_t* __restrict__ tbl, uint32_t* __restrict__ out,
+                                                            uint32_t full, uint32_t S, uint32_t* __restrict__ part_out) {
   constexpr int JW = sizeof(F) / 4 * 3;
   __shared__ uint32_t part[(LG_LANES - 1) * 64 * JW];  // the partial sums of waves 1 .. LG_LANES - 1
   __shared__ uint32_t idxS[64 * LG_LANES][LG_MAXK], lpS[64 * LG_LANES][LG_MAXK], lnS[64 * LG_LANES][LG_MAXK];
-  const int q = (int)(threadIdx.x / 64);  // term lane: wave-uniform
-  const size_t j = (size_t)blockIdx.x * 64 + threadIdx.x % 64;
+  const bool sliced = blockIdx.x >= full;
+  const uint32_t r = blockIdx.x - full;
+  const size_t blk = sliced ? full + r / S : blockIdx.x;
+  const int sl = sliced ? (int)(r % S) : 0, nl = sliced ? (int)S * LG_LANES : LG_LANES;
+  const int q = sl * LG_LANES + (int)(threadIdx.x / 64);  // term lane: wave-uniform
+  const size_t j = blk * 64 + threadIdx.x % 64;
   jac<F> acc = jac_inf<F>();
   if (j < n_rounds && ok[j]) {
     const uint32_t* L = lam + (lam_set ? (size_t)lam_set[j] : j) * t * LAM_WORDS;  // per term: NAF masks, wNAF nibbles
-    const uint32_t* S = sel + j * (size_t)t;
-    const int nt = (t - q + LG_LANES - 1) / LG_LANES;  // terms of this lane: k = q + LG_LANES i
+    const uint32_t* Sel = sel + j * (size_t)t;
+    const int nt = q < t ? (t - q + nl - 1) / nl : 0;  // terms of this lane: k = q + nl i
     // digit masks of the current 32-bit chunk and the point indices live in LDS (dynamic indices, no scratch)
     uint32_t* idx = idxS[threadIdx.x];
     uint32_t* lp = lpS[threadIdx.x];
     uint32_t* ln = lnS[threadIdx.x];
     for (int c0 = 0; c0 < nt; c0 += LG_MAXK) {  // more than LG_MAXK terms: several passes
       const int nc = nt - c0 < LG_MAXK ? nt - c0 : LG_MAXK;
-      for (int i = 0; i < nc; i++) idx[i] = S[q + LG_LANES * (c0 + i)];
+      for (int i = 0; i < nc; i++) idx[i] = Sel[q + nl * (c0 + i)];
       if constexpr (sizeof(F) == sizeof(fp2)) {
-        // a poisoned chain (an exceptional case met by the fast additions) is recomputed by the exact 32-bit chain below
         // width-4 NAF over the partials' tables; a chain that met an exceptional case (poisoned) runs again with
         // the exact formulas
-        j228 a28 = lagrange_wnaf28<false>(L, q, c0, nc, tbl, idx, lp);
-        if (j228_poisoned(a28)) a28 = lagrange_wnaf28<true>(L, q, c0, nc, tbl, idx, lp);
+        j228 a28 = lagrange_wnaf28<false>(L, q, nl, c0, nc, tbl, idx, lp);
+        if (j228_poisoned(a28)) a28 = lagrange_wnaf28<true>(L, q, nl, c0, nc, tbl, idx, lp);
         if (!a28.inf) acc = jac_add(acc, jac<F>{f2_to_fp2(a28.x), f2_to_fp2(a28.y), f2_to_fp2(a28.z)});
         continue;
       }
@@ -419,7 +428,7 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
       for (int b = 255; b >= 0; b--) {
         if ((b & 31) == 31)
           for (int i = 0; i < nc; i++) {
-            const uint32_t* Lk = L + (size_t)(q + LG_LANES * (c0 + i)) * LAM_WORDS;
+            const uint32_t* Lk = L + (size_t)(q + nl * (c0 + i)) * LAM_WORDS;
             lp[i] = Lk[b >> 5];
             ln[i] = Lk[8 + (b >> 5)];
           }
@@ -436,12 +445,23 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
       acc = jac_add(acc, part_acc);
     }
   }
-  if (q) st_jac_aos<F>(part, threadIdx.x - 64, acc);
+  const int w = (int)(threadIdx.x / 64);
+  if (w) st_jac_aos<F>(part, threadIdx.x - 64, acc);
   __syncthreads();
-  if (q == 0 && j < n_rounds) {
-    for (int r = 1; r < LG_LANES; r++) acc = jac_add(acc, ld_jac_aos<F>(part, (size_t)(r - 1) * 64 + threadIdx.x));
-    st_jac_aos<F>(out, j, acc);
+  if (w == 0 && j < n_rounds) {
+    for (int r2 = 1; r2 < LG_LANES; r2++) acc = jac_add(acc, ld_jac_aos<F>(part, (size_t)(r2 - 1) * 64 + threadIdx.x));
+    if (sliced) st_jac_aos<F>(part_out, (j - (size_t)full * 64) * S + sl, acc);
+    else st_jac_aos<F>(out, j, acc);
   }
+}
+template <class F>
+__global__ __launch_bounds__(64) void k_lagrange_sum(const uint32_t* __restrict__ part, uint32_t S, size_t j0, size_t n_rounds,
+                                                     uint32_t* __restrict__ out) {
+  const size_t j = j0 + gtid();
+  if (j >= n_rounds) return;
+  jac<F> acc = ld_jac_aos<F>(part, (j - j0) * S);
+  for (uint32_t s = 1; s < S; s++) acc = jac_add(acc, ld_jac_aos<F>(part, (j - j0) * S + s));
+  st_jac_aos<F>(out, j, acc);
 }
 
 template <class F>
@@ -543,16 +563,43 @@ hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const 
   return hipGetLastError();
 }
 
+static int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v > 0 ? v : 256;
+  }();
+  return n;
+}
+size_t lagrange_tmp_bytes(int sig_g2) { return (size_t)cu_count() * 64 * (sig_g2 ? 72 : 36) * 4; }
+
+template <class F>
+static void lagrange_grid(const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok, int t,
+                          size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, uint32_t* out, uint32_t* tmp,
+                          hipStream_t st) {
+  // one workgroup (LG_LANES waves) per CU at a time: blocks beyond the last full wave of CUs are sliced (k_lagrange)
+  const size_t nb = nblk(n_rounds, 64), ncu = (size_t)cu_count();
+  size_t full = nb, rem = 0, S = 1;
+  const size_t max_s = (size_t)(t + LG_LANES - 1) / LG_LANES;
+  if (tmp && nb > ncu && nb % ncu && nb % ncu <= ncu / 2 && max_s > 1) {
+    rem = nb % ncu;
+    full = nb - rem;
+    S = std::min(max_s, ncu / rem);
+  }
+  hipLaunchKernelGGL(k_lagrange<F>, dim3(full + rem * S), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t, n_rounds,
+                     sig_aff, tbl, out, (uint32_t)full, (uint32_t)S, tmp);
+  if (rem)
+    hipLaunchKernelGGL(k_lagrange_sum<F>, dim3(nblk(n_rounds - full * 64, 64)), dim3(64), 0, st, tmp, (uint32_t)S, full * 64,
+                       n_rounds, out);
+}
+
 hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
                            int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, uint32_t* out,
-                           hipStream_t st) {
+                           uint32_t* tmp, hipStream_t st) {
   if (!n_rounds) return hipSuccess;
-  if (sig_g2)
-    hipLaunchKernelGGL(k_lagrange<fp2>, dim3(nblk(n_rounds, 64)), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t,
-                       n_rounds, sig_aff, tbl, out);
-  else
-    hipLaunchKernelGGL(k_lagrange<fp>, dim3(nblk(n_rounds, 64)), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t,
-                       n_rounds, sig_aff, tbl, out);
+  if (sig_g2) lagrange_grid<fp2>(sel, lam, lam_set, ok, t, n_rounds, sig_aff, tbl, out, tmp, st);
+  else lagrange_grid<fp>(sel, lam, lam_set, ok, t, n_rounds, sig_aff, tbl, out, tmp, st);
   return hipGetLastError();
 }
 

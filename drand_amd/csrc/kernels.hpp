@@ -171,9 +171,11 @@ hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const 
 hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, uint32_t* tbl, uint32_t* zs,
                                 hipStream_t st);
 size_t wnaf_table_scratch_bytes(size_t n);
+// tmp: lagrange_tmp_bytes(sig_g2) of scratch for the sliced last wave of workgroups (null: no slicing)
 hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
                            int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, uint32_t* out,
-                           hipStream_t st);
+                           uint32_t* tmp, hipStream_t st);
+size_t lagrange_tmp_bytes(int sig_g2);
 hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, hipStream_t st);
 hipError_t launch_recover_pairs(int sig_g2, const uint32_t* shares, const uint32_t* B, const uint32_t* A, int n_nodes,
                                 uint32_t* P, uint32_t* Q, hipStream_t st);
