@@ -12,6 +12,7 @@
 #   pmc:<counters>[@<args>] one rocprofv3 --pmc pass of bench.py <args> -> gpurun_out/pmc_<tag>_<i>/
 #   py:<script args>       python <script args>              -> gpurun_out/py_<tag>_<i>.log
 #   env:<NAME>=<value>     export a variable for the steps after it (env:NAME= clears it)
+#   sh:<script args>       bash <script args> (bench/pmc.sh, bench/bisect_sweep.sh: they time-limit their own steps)
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
@@ -59,6 +60,8 @@ for step in "$@"; do
       tail -5 "$O/py_${T}_$i.log" ;;
     env)
       export "$arg" ;;
+    sh)
+      bash $arg ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -99,8 +99,6 @@ struct worker {
   dbuf s28, q28;
   // bisection on the device: the next level's entries, fail flags, their ranks and the scan's block sums
   dbuf entries_alt, cflags, crank, cscan;
-  // bisection from scaled points: [r_i] sigma_i and [r_i] H_i (launch_scale28), the level sums' temporaries
-  dbuf tree_r, tree_a, tree_b;
   // host-API staging
   dbuf in_rounds, in_sigs, in_prevs, in_prev_lens, out_verdict, out_rand;
   // key
@@ -132,8 +130,7 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_zs, &r_tbl, &r_rstat, &r_ltmp, &node_sum, &node_res, &tree_r,
-                   &tree_a, &tree_b};
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_zs, &r_tbl, &r_rstat, &r_ltmp, &node_sum, &node_res};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
     if (tail) (void)hipStreamDestroy(tail);
@@ -525,14 +522,6 @@ static bool lane_pairing() {
   return v;
 }
 
-static bool msm32_selected() {
-  static const bool v = [] {
-    const char* e = getenv("DRANDHIP_MSM32");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 // key_h: [h_eff] pk next to a decoded G2 key (k_decode_key), or null (the check clears B's cofactor itself)
 static hipError_t group_check(worker* w, bool g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key,
                               uint8_t* pass, hipStream_t st, const uint32_t* key_h = nullptr) {
@@ -582,23 +571,21 @@ static const std::vector<size_t>& fixed_ladder() {
 // latency floor), per-round leaf checks ~12 + 0.005 m. Faults are modelled as Poisson at the density the last
 // level observed (faulty groups -> -ln(1 - f) faults per group, at least one per failing group; when every
 // group failed, 5 per group). The next size minimises the expected cost of the rest of the descent.
-static double msm_cost_ms(double m, size_t g, bool tree) {
-  // from scaled points a level's sums are ~1 point addition per entry (launch_group_sums28)
-  if (tree) return 0.5 + 1e-6 * m;
+static double msm_cost_ms(double m, size_t g) {
   const dh::msm_geom gg = geom_for(g, 2);
   return 9.0 + 1.8e-6 * m * (double)(gg.nwin * gg.halves) / 2.0;  // fitted on 127-bit entries (8 per round at c = 16)
 }
 static double check_cost_ms(double groups) { return 12.0 + 0.0025 * groups; }
 static double leaf_cost_ms(double m) { return 12.0 + 0.005 * m; }
 
-static double descent_cost(double m, double d, size_t gprev, size_t* best, bool tree) {
+static double descent_cost(double m, double d, size_t gprev, size_t* best) {
   double c_best = leaf_cost_ms(m);
   if (best) *best = 1;
   for (size_t g = 4; g < gprev && (double)g < m; g *= 4) {
     const double q = -std::expm1(-d * (double)g);  // P(group of g holds a fault)
     const double m_next = m * q;
-    const double c = msm_cost_ms(m, g, tree) + check_cost_ms(m / (double)g) +
-                     (m_next < 1.0 ? 0.0 : descent_cost(m_next, d / std::max(q, 1e-12), g, nullptr, tree));
+    const double c = msm_cost_ms(m, g) + check_cost_ms(m / (double)g) +
+                     (m_next < 1.0 ? 0.0 : descent_cost(m_next, d / std::max(q, 1e-12), g, nullptr));
     if (c < c_best) {
       c_best = c;
       if (best) *best = g;
@@ -607,34 +594,27 @@ static double descent_cost(double m, double d, size_t gprev, size_t* best, bool 
   return c_best;
 }
 
-static size_t next_group_size(size_t gsize, size_t ngroups, size_t nfail, size_t m_prev, size_t m_next, double hint,
-                              bool tree) {
+static size_t next_group_size(size_t gsize, size_t ngroups, size_t nfail, size_t m_prev, size_t m_next, double hint) {
   // level 0 (one group) says only that some round is bad: 1024 costs about what 4096 does over 1M rounds and
   // its groups still pass at a 0.1% fault density (4096-round groups then all fail). When the worker's previous
   // bisection saw dense faults (> 1 per 2000 rounds: most 1024-groups fail), 256-round groups first: the ladder
   // sweep on a 0.2%-faulty chained window put 256-first ladders 5-9% ahead of 1024-first ones
   // (profiles/bisect_sweep_r03s.txt)
   const bool dense = hint > 1.0 / 2000;
-  if (gsize == m_prev && m_prev > 4096 && !tree) return dense ? 256 : 1024;
+  if (gsize == m_prev && m_prev > 4096) return dense ? 256 : 1024;
   // ... and continues 256 -> 32 -> 4 -> per-round leaves, the best ladder of that sweep (231.7 ms per 1M window
   // against 240-259 for the others); the cost model below was fitted on sparser failures
-  if (!tree && dense && (gsize == 256 || gsize == 32)) return gsize == 256 ? 32 : 4;
-  if (!tree && dense && gsize == 4) return 1;
+  if (dense && (gsize == 256 || gsize == 32)) return gsize == 256 ? 32 : 4;
+  if (dense && gsize == 4) return 1;
   const double f = (double)nfail / (double)ngroups;
   const double per_group = nfail == ngroups ? 5.0 : -std::log1p(-f);
   const double faults = std::max((double)nfail, per_group * (double)ngroups);
   const double density = std::min(1.0, faults / (double)std::max<size_t>(m_next, 1));
   size_t g = 1;
-  descent_cost((double)m_next, density, gsize, &g, tree);
+  descent_cost((double)m_next, density, gsize, &g);
   return g;
 }
 
-// Bisection from scaled points (launch_scale28 once per batch, then launch_group_sums28 per level) instead of an MSM
-// per level: OFF by default (DRANDHIP_BISECT_TREE=1 selects it). Measured on the chained 4M replay at 0.1% Cfg5
-// corruption (gpurun_out r04d): 3.45 M beacons/s against 5.34 with the per-level MSMs — k_scale28 took ~430 ms per
-// 1M-round window, because every lane scales its own random scalar: at each bit some lane of the wave has a nonzero
-// NAF digit in every part, so the wave runs every part's addition at nearly every position (~128 additions per point
-// instead of ~41), at one wave per SIMD. The per-level Pippenger keeps the wave uniform.
 static bool prep_sync() {
   static const bool v = [] {
     const char* e = getenv("DRANDHIP_PREP_SYNC");
@@ -652,13 +632,6 @@ static bool skip_level0() {
   return v;
 }
 
-static bool tree_bisection() {
-  static const bool v = [] {
-    const char* e = getenv("DRANDHIP_BISECT_TREE");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
 
 // core pipeline on device-resident inputs
 // Phases of one batch (the node-wide check of dh_batch_begin / dh_batch_finish runs them separately):
@@ -712,28 +685,22 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (stats) memset(stats, 0, 4 * sizeof(uint64_t));
   if (n == 0) return DH_OK;
   // the MSM runs on lazily reduced 28-bit points (k_msm.hip MSM28), whose workspace points take 48 (G1) / 96 (G2)
-  // words; DRANDHIP_MSM32=1 selects the 12 x 32-bit MSM kept as the second implementation. G2 on the 28-bit MSM
-  // splits each scalar in four psi parts, otherwise in two endomorphism halves.
-  const bool msm28 = !msm32_selected();
-  const int parts = g2 && msm28 ? 4 : 2;
+  // words; G2 splits each scalar in four psi parts, G1 in two endomorphism halves. (r01-r03 also kept a 12 x 32-bit
+  // Pippenger behind DRANDHIP_MSM32 as a second implementation; removed in r04, git history has it.)
+  const int parts = g2 ? 4 : 2;
   // sorted-list entries keep a sign bit and address parts * n points (the endomorphism images follow the n points)
   if (n >= ((size_t)1 << 31) / parts) return fail(DH_EINVAL, "batch too large");
   const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
   const size_t aw = jw * 2 / 3;
-  const size_t wsw = msm28 ? (g2 ? 96 : 48) : jw;
+  const size_t wsw = g2 ? 96 : 48;
 
   timed_launches T(st);
   bool presorted = false;  // level-0 sorted lists already built on the tail stream
-  // bisection from scaled points: from level 0 on when this worker's last bisection saw dense faults (> 1 per 2000
-  // rounds: its level 0 is expected to fail, and the scaled points give every level's sums), else once level 0 failed
-  const bool tree_ok = msm28 && tree_bisection();
-  const bool tree_first = tree_ok && mode <= VM_BEGIN && w->fault_density > 1.0 / 2000 && n > 4096;
-  bool tree = tree_first, scaled = false;
   // A local batch on a worker whose last bisection saw dense faults skips level 0: its one group is expected to fail,
   // so the batch starts at the dense ladder's 256-round groups (their check also answers "is the batch clean": a
   // batch whose groups all pass clears the hint). Saves the level-0 MSM and pairing check per dense window.
   // (with a fixed ladder, DRANDHIP_BISECT, its first size)
-  const bool skip0 = !tree_first && mode == VM_FULL && w->fault_density > 1.0 / 2000 && n > 4096 && skip_level0();
+  const bool skip0 = mode == VM_FULL && w->fault_density > 1.0 / 2000 && n > 4096 && skip_level0();
   dh::msm_geom g0{};
   dh::msm_ws ws0{};
   if (mode <= VM_BEGIN) {
@@ -743,8 +710,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
 
     // per-round prep
     HIP_TRY(w->status.ensure(n));
-    HIP_TRY(w->sig_aff.ensure(2 * n * aw * 4));  // points i < n, then their endomorphism images (launch_endo)
-    HIP_TRY(w->q_pts.ensure(2 * n * jw * 4));
+    HIP_TRY(w->sig_aff.ensure(n * aw * 4));
+    HIP_TRY(w->q_pts.ensure(n * jw * 4));
     HIP_TRY(w->scal.ensure(n * 16));
     HIP_TRY(w->entries.ensure(n * 4));
     uint32_t seedw[8];
@@ -753,9 +720,9 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     uint32_t* d_seed = (uint32_t*)((uint8_t*)w->key_ok.p + 32);
     // The level-0 sort needs only the scalars, and the scalars only the seed: with a tail stream it runs there
     // while the per-round kernels decode and hash (its ~1 ms of small kernels left the one-call latency path).
-    // Every round then carries a scalar; the bucket passes skip rounds whose status is not DEC_OK. A worker whose
-    // last bisection saw dense faults takes level 0 from the scaled points instead (no sort).
-    presorted = w->tail && st == w->stream && !tree_first && !skip0;
+    // Every round then carries a scalar; the bucket passes skip rounds whose status is not DEC_OK. A batch that skips
+    // level 0 (skip0) has no level-0 sort.
+    presorted = w->tail && st == w->stream && !skip0;
     if (presorted) {
       hipStream_t ts = w->tail;
       HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, ts));
@@ -783,16 +750,12 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
       HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, st));
       HIP_TRY(dh::launch_scalars(d_seed, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), parts, st));
     }
-    if (msm28) {
-      HIP_TRY(w->s28.ensure(parts * n * (g2 ? 64 : 32) * 4));
-      HIP_TRY(w->q28.ensure(parts * n * (g2 ? 64 : 32) * 4));
-      HIP_TRY(T.run(g2 ? "k_msm_prep28<fp2>" : "k_msm_prep28<fp>", [&] {
-        return dh::launch_msm_prep28(g2, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
-                                     w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), st);
-      }));
-    } else {
-      HIP_TRY(dh::launch_endo(g2, n, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(), st));
-    }
+    HIP_TRY(w->s28.ensure(parts * n * (g2 ? 64 : 32) * 4));
+    HIP_TRY(w->q28.ensure(parts * n * (g2 ? 64 : 32) * 4));
+    HIP_TRY(T.run(g2 ? "k_msm_prep28<fp2>" : "k_msm_prep28<fp>", [&] {
+      return dh::launch_msm_prep28(g2, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
+                                   w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), st);
+    }));
     HIP_TRY(hipMemsetAsync(d_verdict, 0, n, st));
     if (gate) {
       HIP_TRY(hipEventRecord(gate->done, st));
@@ -845,40 +808,16 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     dh::msm_ws ws{};
     if (pre) {
       ws = ws0;
-    } else if (!tree) {  // (tree levels need no MSM workspace: a small-group geometry would size it for every group)
+    } else {
       const int rc = msm_workspace(w, g, m, ngroups, wsw, ws);
       if (rc) return rc;
     }
-    if (tree && !(level == 0 && mode >= VM_FINISH)) {
-      if (!scaled) {  // once per batch: [r_i] sigma_i and [r_i] H_i
-        HIP_TRY(w->tree_r.ensure(dh::scaled_points_bytes(g2, n)));
-        HIP_TRY(T.run("k_scale28", [&] {
-          return dh::launch_scale28(g2, n, w->status.as<uint8_t>(), w->scal.as<uint4>(), w->s28.as<uint32_t>(),
-                                    w->q28.as<uint32_t>(), w->tree_r.as<uint32_t>(), st);
-        }));
-        scaled = true;
-      }
-      const size_t tb = dh::group_sums_tmp_bytes(g2, m, gsize);
-      HIP_TRY(w->tree_a.ensure(tb));
-      HIP_TRY(w->tree_b.ensure(tb));
-      HIP_TRY(w->outA.ensure(ngroups * jw * 4));
-      HIP_TRY(w->outB.ensure(ngroups * jw * 4));
-      HIP_TRY(w->pass.ensure(ngroups));
-      HIP_TRY(T.run(level == 0 ? "tree_sums_level0" : "tree_sums_bisect", [&] {
-        return dh::launch_group_sums28(g2, w->entries.as<uint32_t>(), m, gsize, w->tree_r.as<uint32_t>(), n,
-                                       w->tree_a.as<uint32_t>(), w->tree_b.as<uint32_t>(), w->outA.as<uint32_t>(),
-                                       w->outB.as<uint32_t>(), st);
-      }));
-    } else if (!(level == 0 && mode >= VM_FINISH)) {  // a resumed batch has its level-0 sums from dh_batch_begin
+    if (!(level == 0 && mode >= VM_FINISH)) {  // a resumed batch has its level-0 sums from dh_batch_begin
       // every level skips the rounds whose status is not DEC_OK (their scalars are nonzero after a presort)
       HIP_TRY(T.run(msm_names[std::min(level, 7)], [&] {
-        if (msm28)
-          return dh::launch_msm28(g2, pre ? g0 : g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(),
-                                  w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
-                                  w->outB.as<uint32_t>(), st, w->status.as<uint8_t>(), pre);
-        return dh::launch_msm(g2, pre ? g0 : g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(),
-                              w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
-                              w->outB.as<uint32_t>(), st, w->status.as<uint8_t>(), pre);
+        return dh::launch_msm28(g2, pre ? g0 : g, w->entries.as<uint32_t>(), m, ngroups, w->scal.as<uint4>(),
+                                w->s28.as<uint32_t>(), w->q28.as<uint32_t>(), ws, w->outA.as<uint32_t>(),
+                                w->outB.as<uint32_t>(), st, w->status.as<uint8_t>(), pre);
       }));
     }
     if (level == 0 && mode == VM_BEGIN) return DH_OK;  // queued; dh_batch_begin orders the caller after it
@@ -921,8 +860,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     std::swap(w->entries, w->entries_alt);
     const size_t m_prev = m;
     m = nfail * gsize - (last_pass ? 0 : ngroups * gsize - m_prev);  // only the last group may be short
-    if (tree_ok && m > 1) tree = true;  // the levels below take their sums from the scaled points
-    gsize = fixed.empty() ? next_group_size(gsize, ngroups, nfail, m_prev, m, w->fault_density, tree)
+    gsize = fixed.empty() ? next_group_size(gsize, ngroups, nfail, m_prev, m, w->fault_density)
                           : (size_t)(level - 1 < (int)fixed.size() ? fixed[level - 1] : 1);
   }
   if (m > 0) {

@@ -162,173 +162,10 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_final(const uint32_t* __restric
 // bucket: Poisson(16) sizes at c = 16). A key that lies wholly inside a chunk is written to its bucket
 // directly; a key cut by chunk boundaries leaves partial sums: the chunk where it starts keeps a "tail"
 // partial, each later chunk it covers a "head" partial (kind 1: the key ends in that chunk, kind 2: it
-// covers the whole chunk), and k_msm_bucket_fix adds them up. Buckets of empty keys stay at the zeroed
-// (Z = 0, infinity) value the launcher writes first.
+// covers the whole chunk), and k_msm_bucket_fix28 adds them up. A bucket whose key holds no entry is never read
+// (the reduction tests the key's count).
 constexpr uint32_t NO_KEY = 0xffffffffu;
 
-// skip (optional): per-round status; an entry whose round (point index mod nround: the endomorphism images follow
-// the points) is not DEC_OK adds nothing — the batch check sorts before the rounds are decoded (verify_core), so
-// such rounds carry nonzero scalars
-template <class F, bool AFFINE>
-__global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket(const uint32_t* __restrict__ off, const uint32_t* __restrict__ list,
-                                                    size_t nkeys, uint32_t L, const uint32_t* __restrict__ pts,
-                                                    uint32_t* __restrict__ buckets, uint32_t* __restrict__ part,
-                                                    uint32_t* __restrict__ meta, const uint8_t* __restrict__ skip,
-                                                    uint32_t nround) {
-  const size_t t = gtid();
-  const uint32_t total = off[nkeys];
-  const size_t s = t * (size_t)L;
-  if (s >= total) return;
-  const uint32_t e = (uint32_t)min(s + L, (size_t)total);
-  // the key holding entry s: the largest k with off[k] <= s (off[nkeys] = total > s)
-  size_t lo = 0, hi = nkeys;
-  while (hi - lo > 1) {
-    size_t mid = (lo + hi) >> 1;
-    if (off[mid] <= s) lo = mid;
-    else hi = mid;
-  }
-  size_t key = lo;
-  uint32_t kend = off[key + 1];
-  const bool starts_before = off[key] < s;
-  bool first = true;
-  uint32_t head_kind = 0, tail_key = NO_KEY;
-  jac<F> acc = jac_inf<F>();
-  for (uint32_t j = (uint32_t)s; j < e; j++) {
-    const uint32_t raw = list[j];
-    const uint32_t idx = raw & ~NEG_BIT;
-    const bool neg = (raw & NEG_BIT) != 0;
-    if (!skip || skip[round_of(idx, nround)] == DEC_OK) {
-      if constexpr (AFFINE) {
-        aff<F> pt = ld_aff_aos<F>(pts, idx);
-        pt.y = f_select(neg, f_neg(pt.y), pt.y);
-        acc = jac_add_aff(acc, pt);
-      } else {
-        jac<F> pt = ld_jac_aos<F>(pts, idx);
-        pt.y = f_select(neg, f_neg(pt.y), pt.y);
-        acc = jac_add(acc, pt);
-      }
-    }
-    const bool ends = j + 1 == kend;
-    if (ends || j + 1 == e) {
-      if (first && starts_before) {
-        st_jac_aos<F>(part, 2 * t, acc);
-        head_kind = ends ? 1 : 2;
-      } else if (ends) {
-        st_jac_aos<F>(buckets, key, acc);
-      } else {
-        st_jac_aos<F>(part, 2 * t + 1, acc);
-        tail_key = (uint32_t)key;
-      }
-      first = false;
-      if (ends && j + 1 < e) {  // next non-empty key starts at entry j + 1
-        do {
-          key++;
-        } while (off[key + 1] <= j + 1);
-        kend = off[key + 1];
-        acc = jac_inf<F>();
-      }
-    }
-  }
-  if (meta) {
-    meta[2 * t] = head_kind;
-    meta[2 * t + 1] = tail_key;
-  }
-}
-
-// one thread per chunk that holds a tail partial: add the head partials of the following chunks the key covers
-template <class F>
-__global__ __launch_bounds__(256, occ<F>::W) void k_msm_bucket_fix(const uint32_t* __restrict__ off, size_t nkeys, uint32_t L,
-                                                        const uint32_t* __restrict__ meta, const uint32_t* __restrict__ part,
-                                                        uint32_t* __restrict__ buckets) {
-  const size_t t = gtid();
-  const uint32_t total = off[nkeys];
-  const size_t nch = (total + L - 1) / L;
-  if (t >= nch) return;
-  const uint32_t key = meta[2 * t + 1];
-  if (key == NO_KEY) return;
-  jac<F> acc = ld_jac_aos<F>(part, 2 * t + 1);
-  for (size_t u = t + 1; u < nch; u++) {
-    acc = jac_add(acc, ld_jac_aos<F>(part, 2 * u));
-    if (meta[2 * u] == 1) break;
-  }
-  st_jac_aos<F>(buckets, key, acc);
-}
-
-template <class F, bool AFFINE>
-static hipError_t launch_buckets(const msm_ws& ws, size_t nk, const uint32_t* pts, uint32_t* buckets, uint32_t* part,
-                                 bool write_meta, hipStream_t st, const uint8_t* skip = nullptr, uint32_t nround = 0) {
-  constexpr size_t jw = sizeof(F) / 4 * 3;
-  hipError_t e = hipMemsetAsync(buckets, 0, nk * jw * 4, st);
-  if (e != hipSuccess) return e;
-  if (!ws.max_entries) return hipSuccess;
-  const uint32_t L = msm_chunk_len(ws.max_entries);
-  const size_t nch = (ws.max_entries + L - 1) / L;  // <= msm_nchunks(max_entries): the workspace bound
-  hipLaunchKernelGGL((k_msm_bucket<F, AFFINE>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, ws.list, nk, L, pts, buckets,
-                     part, write_meta ? ws.meta : nullptr, skip, nround);
-  hipLaunchKernelGGL((k_msm_bucket_fix<F>), dim3(nblk(nch, 256)), dim3(256), 0, st, ws.off, nk, L, ws.meta, part, buckets);
-  return hipGetLastError();
-}
-
-// per (group, window, segment): sum_{d in seg} d * B_d via running sums; seg covers digits [a, a + len)
-template <class F>
-__global__ __launch_bounds__(256, occ<F>::W) void k_msm_segsum(const uint32_t* __restrict__ buckets, msm_geom g, size_t ngw,
-                                                    uint32_t* __restrict__ segs) {
-  size_t t = gtid();
-  if (t >= ngw * g.nseg) return;
-  const size_t gw = t / g.nseg;
-  const uint32_t s = t % g.nseg;
-  const uint32_t a = 1 + s * g.seglen;  // first digit of the segment
-  uint32_t last = a + g.seglen;         // exclusive
-  if (last > g.nbuck) last = g.nbuck;
-  jac<F> run = jac_inf<F>(), tot = jac_inf<F>();
-  for (int d = (int)last - 1; d >= (int)a; d--) {
-    run = jac_add(run, ld_jac_aos<F>(buckets, gw * g.nbuck + d));
-    tot = jac_add(tot, run);
-  }
-  // tot = sum (d - a + 1) B_d ; add (a - 1) * run
-  uint32_t k = a - 1;
-  if (k && !jac_is_inf(run)) {
-    jac<F> acc = jac_inf<F>();
-    for (int bit = 31 - __builtin_clz(k); bit >= 0; bit--) {
-      acc = jac_dbl(acc);
-      if ((k >> bit) & 1) acc = jac_add(acc, run);
-    }
-    tot = jac_add(tot, acc);
-  }
-  st_jac_aos<F>(segs, t, tot);
-}
-
-// pairwise tree reduction in place over rows of `stride` points whose first `width` are live:
-// v[r][c] += v[r][c + half] for c + half < width
-template <class F>
-__global__ __launch_bounds__(256, occ<F>::W) void k_msm_tree(uint32_t* __restrict__ v, size_t rows, uint32_t stride, uint32_t width,
-                                                  uint32_t half) {
-  size_t t = gtid();
-  if (t >= rows * half) return;
-  size_t r = t / half, c = t % half;
-  if (c + half >= width) return;
-  size_t i = r * stride + c;
-  st_jac_aos<F>(v, i, jac_add(ld_jac_aos<F>(v, i), ld_jac_aos<F>(v, i + half)));
-}
-
-// per group: Horner over windows, result[g] = sum_w 2^(c w) W_{g,w}; W_{g,w} = segs[(g*nwin + w) * nseg]
-template <class F>
-__global__ __launch_bounds__(64) void k_msm_windows(const uint32_t* __restrict__ segs, msm_geom g, size_t ngroups,
-                                                    uint32_t* __restrict__ out) {
-  size_t t = gtid();
-  if (t >= ngroups) return;
-  jac<F> acc = ld_jac_aos<F>(segs, (t * g.nwin + g.nwin - 1) * g.nseg);
-  for (int w = g.nwin - 2; w >= 0; w--) {
-    for (int k = 0; k < g.c; k++) acc = jac_dbl(acc);
-    acc = jac_add(acc, ld_jac_aos<F>(segs, (t * g.nwin + w) * g.nseg));
-  }
-  st_jac_aos<F>(out, t, acc);
-}
-
-
-// node-wide check (dh_batch_check / dh_check_partials): the records of k batches, each [A | B | status word | pad]
-// (rec_words words), added up: thread 0 sums the A points into outA, thread 1 the B points into outB, thread 2 ORs
-// the ranks' status words into *flag (nonzero: some rank abandoned the batch)
 template <class F>
 __global__ __launch_bounds__(64) void k_sum_partials(const uint32_t* __restrict__ parts, size_t k, size_t rec_words,
                                                      uint32_t* __restrict__ outA, uint32_t* __restrict__ outB,
@@ -400,21 +237,6 @@ hipError_t launch_scan(const uint32_t* cnt, size_t nk, uint32_t* off, uint32_t* 
 }
 
 
-template <class F>
-static hipError_t msm_reduce(const msm_geom& g, size_t ngroups, uint32_t* buckets, uint32_t* segs, uint32_t* out,
-                             hipStream_t st) {
-  size_t ngw = ngroups * g.nwin;
-  hipLaunchKernelGGL(k_msm_segsum<F>, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, buckets, g, ngw, segs);
-  for (uint32_t width = g.nseg; width > 1;) {
-    uint32_t half = (width + 1) / 2;
-    hipLaunchKernelGGL(k_msm_tree<F>, dim3(nblk(ngw * half, 256)), dim3(256), 0, st, segs, ngw, g.nseg, width, half);
-    width = half;  // live prefix of each row; the row stride stays nseg
-  }
-  hipLaunchKernelGGL(k_msm_windows<F>, dim3(nblk(ngroups, 64)), dim3(64), 0, st, segs, g, ngroups, out);
-  return hipGetLastError();
-}
-
-
 hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp, size_t m,
                            size_t ngroups, const uint4* scal, msm_ws& ws, hipStream_t st) {
   size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
@@ -426,51 +248,6 @@ hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32
   if ((e = hipMemcpyAsync(ws.cnt, ws.off, nk * sizeof(uint32_t), hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
   if (m) hipLaunchKernelGGL(k_msm_scatter, dim3(nblk(m, 256)), dim3(256), 0, st, pidx, sidx, grp, m, scal, g, ws.cnt, ws.list);
   return hipGetLastError();
-}
-
-// point set of the sorted lists: field (G1 / G2) and representation (affine AoS / Jacobian AoS)
-hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngroups, const uint32_t* pts, msm_ws& ws,
-                             uint32_t* out, hipStream_t st) {
-  size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
-  hipError_t e;
-  if (g2) {
-    e = affine ? launch_buckets<fp2, true>(ws, nk, pts, ws.buckets, ws.part, true, st)
-               : launch_buckets<fp2, false>(ws, nk, pts, ws.buckets, ws.part, true, st);
-    if (e != hipSuccess) return e;
-    return msm_reduce<fp2>(g, ngroups, ws.buckets, ws.segs, out, st);
-  }
-  e = affine ? launch_buckets<fp, true>(ws, nk, pts, ws.buckets, ws.part, true, st)
-             : launch_buckets<fp, false>(ws, nk, pts, ws.buckets, ws.part, true, st);
-  if (e != hipSuccess) return e;
-  return msm_reduce<fp>(g, ngroups, ws.buckets, ws.segs, out, st);
-}
-
-// both point sets of the RLC check in one pass: the buckets of sigma (affine) and of the hash points
-// (Jacobian) sit back to back, so the reduction kernels run once over 2 x ngroups groups (twice the
-// threads in every latency-bound reduction step instead of two serial passes).
-hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
-                      const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
-                      hipStream_t st, const uint8_t* skip, bool presorted) {
-  hipError_t e = hipSuccess;
-  if (!presorted && (e = launch_msm_sort(g, entries, nullptr, nullptr, m, ngroups, scal, ws, st)) != hipSuccess) return e;
-  const size_t nk = ngroups * g.nwin * (size_t)g.nbuck;
-  const size_t jw = sig_g2 ? 72 : 36;
-  uint32_t* bB = ws.buckets + nk * jw;
-  // the partial sums of the two point sets sit back to back; the chunk metadata is the same for both
-  uint32_t* pB = ws.part + msm_nchunks(ws.max_entries) * 2 * jw;
-  if (sig_g2) {
-    if ((e = launch_buckets<fp2, true>(ws, nk, sig_aff, ws.buckets, ws.part, true, st, skip, g.half_stride)) != hipSuccess) return e;
-    if ((e = launch_buckets<fp2, false>(ws, nk, q_pts, bB, pB, false, st, skip, g.half_stride)) != hipSuccess) return e;
-    e = msm_reduce<fp2>(g, 2 * ngroups, ws.buckets, ws.segs, ws.out2, st);
-  } else {
-    if ((e = launch_buckets<fp, true>(ws, nk, sig_aff, ws.buckets, ws.part, true, st, skip, g.half_stride)) != hipSuccess) return e;
-    if ((e = launch_buckets<fp, false>(ws, nk, q_pts, bB, pB, false, st, skip, g.half_stride)) != hipSuccess) return e;
-    e = msm_reduce<fp>(g, 2 * ngroups, ws.buckets, ws.segs, ws.out2, st);
-  }
-  if (e != hipSuccess) return e;
-  const size_t bytes = ngroups * jw * 4;
-  if ((e = hipMemcpyAsync(outA, ws.out2, bytes, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
-  return hipMemcpyAsync(outB, ws.out2 + ngroups * jw, bytes, hipMemcpyDeviceToDevice, st);
 }
 
 // ================================================================ the RLC MSM in the lazily reduced 28-bit form
@@ -734,7 +511,10 @@ DH_DEV typename C::P bucket_add(const typename C::P& acc, const uint32_t* __rest
   }
 }
 
-// the balanced bucket pass of k_msm_bucket (same chunking, partials and metadata) on 28-bit points
+// the balanced bucket pass (chunks of the sorted list, head / tail partials and their metadata, above) on 28-bit
+// points. skip (optional): per-round status; an entry whose round (point index mod nround: the endomorphism images
+// follow the points) is not DEC_OK adds nothing — the batch check sorts before the rounds are decoded (verify_core),
+// so such rounds carry nonzero scalars
 template <class C, bool AFFINE>
 __global__ __launch_bounds__(256, C::OCC) void k_msm_bucket28(const uint32_t* __restrict__ off, const uint32_t* __restrict__ list,
                                                          size_t nkeys, uint32_t L, const uint32_t* __restrict__ pts,
@@ -989,190 +769,6 @@ hipError_t launch_msm28(int sig_g2, const msm_geom& g, const uint32_t* entries, 
   const size_t ow = sig_g2 ? 72 : 36, bytes = ngroups * ow * 4;
   if ((e = hipMemcpyAsync(outA, ws.out2, bytes, hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
   return hipMemcpyAsync(outB, ws.out2 + ngroups * ow, bytes, hipMemcpyDeviceToDevice, st);
-}
-
-// ================================================================ bisection from per-round scaled points
-// A batch whose level-0 check fails is bisected: every later level needs, per group G of its compacted entries,
-// A_G = sum_{i in G} r_i sigma_i and B_G = sum_{i in G} r_i H_i with the level-0 scalars. Instead of a grouped Pippenger
-// MSM per level (whose per-group bucket reduction dominates at small groups: a 64-round group cost ~4x the per-round
-// work of level 0), the scaled points R_i = [r_i] sigma_i and T_i = [r_i] H_i are computed ONCE per batch (k_scale28,
-// one lane per point: a joint double-and-add over the endomorphism parts of r_i with NAF digits of each part, on the
-// same 28-bit lazy points and formulas as the MSM), and each level's sums are segmented additions over the entries
-// (k_gsum28 + k_rowsum28): ~1 point addition per entry per level. The sums are the same group elements the MSM
-// computes (sum over parts h of [part_h] endo^h(P)), so verdicts do not depend on the path.
-template <class C>
-DH_DEV uint64_t part_value(const uint4& s, int h) {
-  if constexpr (C::PARTS == 4) return h == 0 ? s.x : h == 1 ? s.y : h == 2 ? s.z : s.w;  // 31-bit parts
-  else return h ? ((uint64_t)s.w << 32 | s.z) : ((uint64_t)s.y << 32 | s.x);             // 63-bit halves
-}
-// non-adjacent form of k < 2^63 as two digit masks: digit i = +1 at pos bit i, -1 at neg bit i (from 3k: the NAF's
-// nonzero digits sit where 3k and k differ, shifted down one; positions 0..63)
-DH_DEV void naf_masks(uint64_t k, uint64_t& pos, uint64_t& neg) {
-  const uint64_t k2 = k << 1, lo = k + k2;
-  const uint64_t c = lo < k2 ? 1 : 0;  // bit 64 of 3k
-  pos = ((lo & ~k) >> 1) | (c << 63);
-  neg = (~lo & k) >> 1;
-}
-template <class C, bool EXACT>
-DH_DEV typename C::P scale_run(const uint32_t* __restrict__ pts, size_t n, size_t i, const uint64_t* pos, const uint64_t* neg,
-                               int top) {
-  typename C::P acc = C::inf();
-#pragma unroll 1
-  for (int b = top; b >= 0; b--) {
-    if (!acc.inf) acc = C::dbl(acc);
-#pragma unroll 1
-    for (int h = 0; h < C::PARTS; h++) {
-      const bool dp = (pos[h] >> b) & 1, dn = (neg[h] >> b) & 1;
-      if (dp || dn) {
-        const uint32_t* pt = pts + 2 * C::EW * (h * n + i);
-        typename C::E x, y;
-        ld28(x, pt);
-        ld28(y, pt + C::EW);
-        if (dn) y = C::neg(y);
-        acc = EXACT ? C::madd(acc, x, y) : C::madd_fast(acc, x, y);
-      }
-    }
-  }
-  return acc;
-}
-// R[t] for t < n: [r_t] sigma_t; R[n + i]: [r_i] H_i (lazy Jacobian, identity for a round whose status is not DEC_OK)
-template <class C>
-__global__ __launch_bounds__(256, C::OCC) void k_scale28(size_t n, const uint8_t* __restrict__ status, const uint4* __restrict__ scal,
-                                                         const uint32_t* __restrict__ S, const uint32_t* __restrict__ Q,
-                                                         uint32_t* __restrict__ R) {
-  const size_t t = gtid();
-  if (t >= 2 * n) return;
-  const size_t i = t < n ? t : t - n;
-  typename C::P acc = C::inf();
-  if (status[i] == DEC_OK) {
-    const uint4 s = scal[i];
-    uint64_t pos[C::PARTS], neg[C::PARTS], any = 0;
-#pragma unroll
-    for (int h = 0; h < C::PARTS; h++) {
-      naf_masks(part_value<C>(s, h), pos[h], neg[h]);
-      any |= pos[h] | neg[h];
-    }
-    if (any) {
-      const int top = 63 - __builtin_clzll(any);
-      const uint32_t* pts = t < n ? S : Q;
-      acc = scale_run<C, false>(pts, n, i, pos, neg, top);
-      if (C::poisoned(acc)) acc = scale_run<C, true>(pts, n, i, pos, neg, top);
-    }
-  }
-  stj28<C>(R, t, acc);
-}
-
-// level sums, pass 1: one lane per (set, group, chunk of up to L entries of the group); out row (set * ngroups + g),
-// column c, cpg columns per row
-template <class C, bool EXACT>
-DH_DEV typename C::P chunk_sum(const uint32_t* __restrict__ entries, size_t a, size_t b, const uint32_t* __restrict__ R,
-                               size_t base) {
-  typename C::P acc = C::inf();
-#pragma unroll 1
-  for (size_t e = a; e < b; e++) acc = C::template add_mem<EXACT>(acc, R + (size_t)3 * C::EW * (base + entries[e]));
-  return acc;
-}
-template <class C>
-__global__ __launch_bounds__(256, C::OCC) void k_gsum28(const uint32_t* __restrict__ entries, size_t m, size_t gsize,
-                                                        size_t ngroups, uint32_t L, uint32_t cpg, const uint32_t* __restrict__ R,
-                                                        size_t n, uint32_t* __restrict__ out) {
-  const size_t t = gtid();
-  const size_t per_set = ngroups * cpg;
-  if (t >= 2 * per_set) return;
-  const size_t set = t / per_set, r = t % per_set, g = r / cpg, c = r % cpg;
-  const size_t g0 = g * gsize, gend = min(m, g0 + gsize);
-  const size_t a = g0 + c * (size_t)L, b = min(gend, a + L);
-  typename C::P acc = C::inf();
-  if (a < b) {
-    acc = chunk_sum<C, false>(entries, a, b, R, set * n);
-    if (C::poisoned(acc)) acc = chunk_sum<C, true>(entries, a, b, R, set * n);
-  }
-  stj28<C>(out, t, acc);
-}
-// pass 2..: each lane adds up to `fan` consecutive columns of a row; the last pass (one column left) writes the
-// 12 x 32-bit Montgomery Jacobian the group checks read: rows < ngroups to outA, the others to outB
-template <class C, bool EXACT>
-DH_DEV typename C::P cols_sum(const uint32_t* __restrict__ in, size_t a, size_t b) {
-  typename C::P acc = ldj28<C>(in, a);
-#pragma unroll 1
-  for (size_t k = a + 1; k < b; k++) acc = C::template add_mem<EXACT>(acc, in + (size_t)3 * C::EW * k);
-  return acc;
-}
-template <class C>
-__global__ __launch_bounds__(256, C::OCC) void k_rowsum28(const uint32_t* __restrict__ in, size_t rows, uint32_t cnt, uint32_t fan,
-                                                          uint32_t* __restrict__ out, size_t ngroups, uint32_t* __restrict__ outA,
-                                                          uint32_t* __restrict__ outB) {
-  const size_t t = gtid();
-  const uint32_t cnt_out = (cnt + fan - 1) / fan;
-  if (t >= rows * cnt_out) return;
-  const size_t r = t / cnt_out, j = t % cnt_out;
-  const size_t a = r * cnt + j * (size_t)fan, b = r * cnt + min((size_t)cnt, (j + 1) * (size_t)fan);
-  typename C::P acc = cols_sum<C, false>(in, a, b);
-  if (C::poisoned(acc)) acc = cols_sum<C, true>(in, a, b);
-  if (cnt_out > 1) {
-    stj28<C>(out, t, acc);
-    return;
-  }
-  jac<typename C::F> q = jac_inf<typename C::F>();
-  if (!acc.inf) {
-    q.x = C::out(acc.x);
-    q.y = C::out(acc.y);
-    q.z = C::out(acc.z);
-  }
-  st_jac_aos<typename C::F>(r < ngroups ? outA : outB, r < ngroups ? r : r - ngroups, q);
-}
-
-size_t scaled_points_bytes(int sig_g2, size_t n) { return 2 * n * 3 * (sig_g2 ? 2 * W28 : W28) * 4; }
-
-hipError_t launch_scale28(int sig_g2, size_t n, const uint8_t* status, const uint4* scal, const uint32_t* S, const uint32_t* Q,
-                          uint32_t* R, hipStream_t st) {
-  if (!n) return hipSuccess;
-  if (sig_g2) hipLaunchKernelGGL(k_scale28<c28_g2>, dim3(nblk(2 * n, 256)), dim3(256), 0, st, n, status, scal, S, Q, R);
-  else hipLaunchKernelGGL(k_scale28<c28_g1>, dim3(nblk(2 * n, 256)), dim3(256), 0, st, n, status, scal, S, Q, R);
-  return hipGetLastError();
-}
-
-// chunk length of pass 1: about 2 x 131,072 lanes over both sets, at most 32 entries, within a group
-static uint32_t gsum_chunk(size_t m, size_t gsize) {
-  size_t L = 2 * m / 262144;
-  if (L < 1) L = 1;
-  if (L > 32) L = 32;
-  if (L > gsize) L = gsize;
-  return (uint32_t)L;
-}
-size_t group_sums_tmp_bytes(int sig_g2, size_t m, size_t gsize) {
-  const size_t ngroups = (m + gsize - 1) / gsize, L = gsum_chunk(m, gsize), cpg = (gsize + L - 1) / L;
-  return 2 * ngroups * cpg * 3 * (sig_g2 ? 2 * W28 : W28) * 4;
-}
-
-template <class C>
-static hipError_t group_sums28(const uint32_t* entries, size_t m, size_t gsize, const uint32_t* R, size_t n, uint32_t* tmpA,
-                               uint32_t* tmpB, uint32_t* outA, uint32_t* outB, hipStream_t st) {
-  const size_t ngroups = (m + gsize - 1) / gsize;
-  const uint32_t L = gsum_chunk(m, gsize);
-  uint32_t cnt = (uint32_t)((gsize + L - 1) / L);
-  const size_t rows = 2 * ngroups;
-  hipLaunchKernelGGL(k_gsum28<C>, dim3(nblk(rows * cnt, 256)), dim3(256), 0, st, entries, m, gsize, ngroups, L, cnt, R, n, tmpA);
-  uint32_t* in = tmpA;
-  uint32_t* out = tmpB;
-  for (;;) {
-    const uint32_t fan = 16, cnt_out = (cnt + fan - 1) / fan;
-    hipLaunchKernelGGL(k_rowsum28<C>, dim3(nblk(rows * cnt_out, 256)), dim3(256), 0, st, in, rows, cnt, fan, out, ngroups, outA,
-                       outB);
-    if (cnt_out == 1) break;
-    cnt = cnt_out;
-    uint32_t* sw = in;
-    in = out;
-    out = sw;
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_group_sums28(int sig_g2, const uint32_t* entries, size_t m, size_t gsize, const uint32_t* R, size_t n,
-                               uint32_t* tmpA, uint32_t* tmpB, uint32_t* outA, uint32_t* outB, hipStream_t st) {
-  if (!m) return hipSuccess;
-  return sig_g2 ? group_sums28<c28_g2>(entries, m, gsize, R, n, tmpA, tmpB, outA, outB, st)
-                : group_sums28<c28_g1>(entries, m, gsize, R, n, tmpA, tmpB, outA, outB, st);
 }
 
 // one point set of 28-bit points (launch_msm_prep28): entry e is point pidx[e] (+ its endomorphism images at

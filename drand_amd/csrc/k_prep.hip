@@ -6,7 +6,7 @@
 //   k_prep_msg     DigestBeacon + hash_to_curve without cofactor clearing               [A2, A3, A4b]
 //   k_scalars      128-bit random-linear-combination scalars r_i = SHA-256(seed || i)   [batching, new]
 //   MSM (grouped Pippenger, shared sort for both point sets):
-//     k_msm_hist -> scan -> k_msm_scatter -> k_msm_bucket<S>, k_msm_bucket<Q> -> k_msm_segsum -> k_msm_tree
+//     k_msm_hist -> scan -> k_msm_scatter -> k_msm_bucket28<S>, k_msm_bucket28<Q> -> k_msm_segsum28 -> k_msm_tree28
 //     -> k_msm_windows       per group g:  A_g = sum r_i sigma_i,  B_g = sum r_i Q_i
 //   k_group_check  e(A_g, g2) == e([h_eff] B_g, pk)  (or the G2-signature mirror), one lane per group [A4c]
 //   k_leaf_check   per-round 2-pairing check for rounds left in failing groups (bisection leaves)
@@ -179,26 +179,6 @@ __global__ __launch_bounds__(256) void k_scalars(const uint32_t* __restrict__ se
   scal[i] = r;
 }
 
-// endomorphism images of the batch's points for the split MSM (G1: phi, one Fp product; G2: psi)
-template <class F>
-__global__ __launch_bounds__(256, occ<F>::W) void k_endo(size_t n, uint32_t* __restrict__ sig_aff, uint32_t* __restrict__ q_pts) {
-  size_t i = gtid();
-  if (i >= n) return;
-  aff<F> a = ld_aff_aos<F>(sig_aff, i);
-  jac<F> q = ld_jac_aos<F>(q_pts, i);
-  if constexpr (sizeof(F) == sizeof(fp)) {
-    a.x = fp_mul(a.x, fp_c(cst::BETA));
-    q.x = fp_mul(q.x, fp_c(cst::BETA));
-  } else {
-    a.x = fp2_mul(fp2_conj(a.x), fp2_c(cst::PSI_X));
-    a.y = fp2_mul(fp2_conj(a.y), fp2_c(cst::PSI_Y));
-    q = g2_psi(q);
-  }
-  st_aff_aos<F>(sig_aff, n + i, a);
-  st_jac_aos<F>(q_pts, n + i, q);
-}
-
-
 // ---------------------------------------------------------------- key decode (one thread)
 template <class K>
 __global__ void k_decode_key(const uint8_t* __restrict__ pk, uint32_t* __restrict__ key_aff, uint8_t* __restrict__ ok) {
@@ -240,14 +220,6 @@ hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* s
   hipLaunchKernelGGL(k_scalars, dim3(nblk(n, 256)), dim3(256), 0, st, seed_words, n, status, parts, scal);
   return hipGetLastError();
 }
-
-hipError_t launch_endo(int sig_g2, size_t n, uint32_t* sig_aff, uint32_t* q_pts, hipStream_t st) {
-  if (!n) return hipSuccess;
-  if (sig_g2) hipLaunchKernelGGL(k_endo<fp2>, dim3(nblk(n, 256)), dim3(256), 0, st, n, sig_aff, q_pts);
-  else hipLaunchKernelGGL(k_endo<fp>, dim3(nblk(n, 256)), dim3(256), 0, st, n, sig_aff, q_pts);
-  return hipGetLastError();
-}
-
 
 hipError_t launch_decode_key(int key_g2, const uint8_t* pk, uint32_t* key_aff, uint8_t* ok, hipStream_t st) {
   if (key_g2) hipLaunchKernelGGL(k_decode_key<fp2>, dim3(1), dim3(64), 0, st, pk, key_aff, ok);

@@ -33,10 +33,10 @@ struct msm_ws {
   uint32_t* off;       // nkeys + 1
   uint32_t* scan_tmp;  // ceil(nkeys / 4096)
   uint32_t* list;      // msm_entries(g, m)
-  uint32_t* buckets;   // nkeys Jacobian points (x2 for launch_msm: both point sets)
-  uint32_t* segs;      // ngroups * nwin * nseg Jacobian points (x2 for launch_msm)
-  uint32_t* out2;      // launch_msm: 2 * ngroups Jacobian points (sigma sums, then hash sums)
-  uint32_t* part;      // balanced bucket pass: 2 Jacobian partial sums per chunk (x2 for launch_msm)
+  uint32_t* buckets;   // nkeys Jacobian points (x2 for launch_msm28: both point sets)
+  uint32_t* segs;      // ngroups * nwin * nseg Jacobian points (x2 for launch_msm28)
+  uint32_t* out2;      // launch_msm28: 2 * ngroups Jacobian points (sigma sums, then hash sums)
+  uint32_t* part;      // balanced bucket pass: 2 Jacobian partial sums per chunk (x2 for launch_msm28)
   uint32_t* meta;      // balanced bucket pass: 2 words per chunk (head kind, tail key)
   size_t max_entries;  // set by launch_msm_sort: upper bound of sorted-list entries (msm_entries)
   uint32_t* runs = nullptr;  // MSM28: the segments' running sums (as many points as segs)
@@ -74,21 +74,13 @@ hipError_t launch_hash(int sig_g2, const uint64_t* rounds, const uint8_t* prevs,
 // 0 for rounds whose status is not DEC_OK (status null: every round gets its scalar)
 // parts: 1 = one 127-bit scalar, 2 = two 63-bit halves, 4 = four 31-bit parts (msm_geom halves)
 hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* status, uint4* scal, int parts, hipStream_t st);
-// endomorphism images for the split MSM: sig_aff[n + i] = endo(sig_aff[i]), q_pts[n + i] = endo(q_pts[i])
-// (G1: phi(x, y) = (beta x, y); G2: psi), so the sorted lists address them as point n + i
-hipError_t launch_endo(int sig_g2, size_t n, uint32_t* sig_aff, uint32_t* q_pts, hipStream_t st);
 hipError_t launch_decode_key(int key_g2, const uint8_t* pk, uint32_t* key_aff, uint8_t* ok, hipStream_t st);
 hipError_t launch_iota(uint32_t* v, size_t n, hipStream_t st);
 hipError_t launch_scan(const uint32_t* cnt, size_t nk, uint32_t* off, uint32_t* tmp, hipStream_t st);
-// skip (optional): per-round status, entries of rounds not DEC_OK add nothing (point index mod g.half_stride);
-// presorted: the sorted lists of (entries, scal) are already in ws (launch_msm_sort on the same geometry)
-hipError_t launch_msm(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
-                      const uint32_t* sig_aff, const uint32_t* q_pts, msm_ws& ws, uint32_t* outA, uint32_t* outB,
-                      hipStream_t st, const uint8_t* skip = nullptr, bool presorted = false);
-// the same MSM on the lazily reduced 28-bit points (k_msm.hip MSM28): launch_msm_prep28 converts the batch's sigma
+// The RLC MSM on lazily reduced 28-bit points (k_msm.hip MSM28): launch_msm_prep28 converts the batch's sigma
 // (affine) and hash points (Jacobian, made affine) with their endomorphism images into S and Q (G1 32 / G2 64 words
-// per point, 2n points each; a hash point at infinity marks its round DEC_BAD); the workspace's bucket / partial /
-// segment arrays hold 48 / 96-word Jacobian points
+// per point, parts x n points each: the images of point i at i + h n; a hash point at infinity marks its round
+// DEC_BAD); the workspace's bucket / partial / segment arrays hold 48 / 96-word Jacobian points
 hipError_t launch_msm_prep28(int sig_g2, size_t n, uint8_t* status, const uint32_t* sig_aff, const uint32_t* q_pts,
                              uint32_t* S, uint32_t* Q, hipStream_t st, uint32_t sets = 3);
 // one point set (S of launch_msm_prep28) with point / scalar / group indices: ngroups 12 x 32-bit Jacobian sums into out
@@ -100,8 +92,6 @@ hipError_t launch_msm28(int sig_g2, const msm_geom& g, const uint32_t* entries, 
                         const uint8_t* skip, bool presorted);
 hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32_t* sidx, const uint32_t* grp, size_t m,
                            size_t ngroups, const uint4* scal, msm_ws& ws, hipStream_t st);
-hipError_t launch_msm_points(int g2, int affine, const msm_geom& g, size_t ngroups, const uint32_t* pts, msm_ws& ws,
-                             uint32_t* out, hipStream_t st);
 hipError_t launch_group_check(int sig_g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_aff,
                               uint8_t* pass, hipStream_t st);
 // node-wide check: sum the k (A, B) level-0 partial-sum pairs, record i = [A_i | B_i | status word | pad] at
@@ -113,15 +103,6 @@ hipError_t launch_sum_partials(int sig_g2, const uint32_t* parts, size_t k, size
 hipError_t launch_node_mark(size_t n, uint8_t* res, const uint8_t* status, uint8_t* verdict, hipStream_t st);
 hipError_t launch_mark_groups(const uint32_t* entries, size_t m, size_t gsize, const uint8_t* pass, const uint8_t* status,
                               uint8_t* verdict, hipStream_t st);
-// bisection from per-round scaled points (k_msm.hip): R = 2n lazy Jacobian points ([r_i] sigma_i, then [r_i] H_i) of the
-// 28-bit points of launch_msm_prep28; then per level the group sums of the entries (groups of gsize consecutive
-// entries) into outA / outB (12 x 32-bit Jacobian), with two temporaries of group_sums_tmp_bytes
-size_t scaled_points_bytes(int sig_g2, size_t n);
-hipError_t launch_scale28(int sig_g2, size_t n, const uint8_t* status, const uint4* scal, const uint32_t* S, const uint32_t* Q,
-                          uint32_t* R, hipStream_t st);
-size_t group_sums_tmp_bytes(int sig_g2, size_t m, size_t gsize);
-hipError_t launch_group_sums28(int sig_g2, const uint32_t* entries, size_t m, size_t gsize, const uint32_t* R, size_t n,
-                               uint32_t* tmpA, uint32_t* tmpB, uint32_t* outA, uint32_t* outB, hipStream_t st);
 // bisection: out = the entries of the groups with pass == 0, in order; rank[ngroups] = the number of failing groups
 // (flags: ngroups words, rank: ngroups + 1, scan_tmp: launch_scan's)
 hipError_t launch_compact_failing(const uint32_t* entries, size_t m, size_t gsize, size_t ngroups, const uint8_t* pass,

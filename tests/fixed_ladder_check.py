@@ -1,6 +1,5 @@
 """Child process for tests/test_gpu_parity.py::test_fixed_bisection_ladder: with DRANDHIP_BISECT set by the parent
-(a fixed ladder of group sizes instead of the expected-cost choice) and DRANDHIP_BISECT_TREE (bisection sums from
-per-round scaled points, or an MSM per level), verifies a quicknet batch with 0.5% corrupted rounds twice, then a G2 (pedersen-bls-unchained) batch with one forged round through the device entry point, and prints
+(a fixed ladder of group sizes instead of the expected-cost choice) and DRANDHIP_SKIP_LEVEL0, verifies a quicknet batch with 0.5% corrupted rounds twice, then a G2 (pedersen-bls-unchained) batch with one forged round through the device entry point, and prints
 the rejected indices, the expected sets and the G2 batch statistics as JSON."""
 import hashlib
 import json
@@ -31,8 +30,8 @@ for k, i in enumerate(bad):
         sigs[i, 0] ^= 0x20
 v, _ = s.verify_beacons(pk, rounds, sigs, seed=21)
 out = {"rejected": np.flatnonzero(~v).tolist(), "expected": bad.tolist()}
-# the same batch again: the worker's first bisection saw dense faults (0.5%), so with the scaled-point bisection
-# (DRANDHIP_BISECT_TREE=1) this call takes level 0 from the scaled points too (no level-0 MSM)
+# the same batch again: the worker's first bisection saw dense faults (0.5%), so this call skips level 0 and starts
+# at the ladder's first size (unless DRANDHIP_SKIP_LEVEL0=0)
 v2, _ = s.verify_beacons(pk, rounds, sigs, seed=22)
 out["rejected_again"] = np.flatnonzero(~v2).tolist()
 

@@ -337,17 +337,17 @@ def test_one_lane_pairing_path(dh):
         assert v == [x["valid"] for x in neg[name]["cases"]], name
 
 
-@pytest.mark.parametrize("tree", ["1", "0"])
+@pytest.mark.parametrize("skip0", ["1", "0"])
 @pytest.mark.parametrize("ladder", ["4096,256,16,2", "64"])
-def test_fixed_bisection_ladder(dh, ladder, tree):
+def test_fixed_bisection_ladder(dh, ladder, skip0):
     """The bisection is exact whatever the group sizes: a fixed ladder (DRANDHIP_BISECT, the r01 sizes with the
     c = 10 window geometry, and a single level of 64 before leaves) rejects exactly the corrupted rounds, as the
-    default expected-cost ladder does in the tests above — with the level sums taken from per-round scaled points
-    (tree "1", opt-in; the second quicknet call, after a dense first one, also takes level 0 from them) and from a
-    grouped MSM per level (tree "0", the default). The G2 statistics pin the sums themselves: exactly one failing group per level."""
+    default expected-cost ladder does in the tests above. The second quicknet call comes after a dense first one, so
+    with skip0 "1" (the default) it starts at the ladder's first size without a level-0 check, with "0" it runs level 0
+    first. The G2 statistics pin the sums themselves: exactly one failing group per level."""
     import subprocess
     import sys
-    env = dict(os.environ, DRANDHIP_BISECT=ladder, DRANDHIP_BISECT_TREE=tree)
+    env = dict(os.environ, DRANDHIP_BISECT=ladder, DRANDHIP_SKIP_LEVEL0=skip0)
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "fixed_ladder_check.py")],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]

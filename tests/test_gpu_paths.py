@@ -513,7 +513,7 @@ def test_group_checks_pass_on_clean_batches(dh, scheme):
     So the batch statistics are checked: a clean batch (with one undecodable round, scalar 0) passes its single
     level-0 group check, and a batch with one forged round fails exactly one group per bisection level and sends
     at most a handful of rounds to leaves. This pins the random-linear-combination sums, including the
-    endomorphism split (scalars a + b*mu with endo(P) images, k_endo) at every level."""
+    endomorphism split (scalars a + b*mu with endo(P) images, k_msm_prep28) at every level."""
     import ctypes
     import torch
     from drand_amd import _lib

@@ -1,0 +1,40 @@
+"""Model (CPU, test infrastructure) of the width-4 NAF recoding of the tbls Lagrange coefficients (drand_amd/csrc/fr.hpp
+fr_wnaf4, written by k_select_lagrange and decoded by k_recover.hip lagrange_wnaf28)."""
+import random
+
+
+def wnaf4_nibbles(k):
+    """fr.hpp fr_wnaf4: 256 nibbles (v in 1..4 = +(2v - 1), 9..12 = -(2(v - 8) - 1)), little-endian positions"""
+    out = []
+    for _ in range(256):
+        v = 0
+        if k & 1:
+            d = k & 15
+            if d >= 8:
+                d -= 16
+            k -= d
+            v = (d + 1) // 2 if d > 0 else 8 + (1 - d) // 2
+        k >>= 1
+        out.append(v)
+    assert k == 0
+    return out
+
+
+def test_wnaf4_digits():
+    """The Lagrange coefficients' width-4 NAF as k_lagrange decodes it: digit (v & 7) selects table entry
+    (v & 7) - 1 of {P, 3P, 5P, 7P}, bit 8 the sign; sum d_b 2^b == lambda, odd digits in [-7, 7], >= 3 zeros after
+    each nonzero digit, for lambda < r."""
+    R = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    rng = random.Random(11)
+    for lam in [1, 7, 8, 15, 16, 255, R - 1, R - 2, (1 << 254) + 3] + [rng.randrange(R) for _ in range(3000)]:
+        nib = wnaf4_nibbles(lam)
+        total, last = 0, -10
+        for b, v in enumerate(nib):
+            if not v:
+                continue
+            assert v in (1, 2, 3, 4, 9, 10, 11, 12)
+            mag = 2 * (v & 7) - 1
+            total += (-mag if v & 8 else mag) << b
+            assert b - last >= 4
+            last = b
+        assert total == lam
