@@ -215,12 +215,16 @@ DH_DEV j228 j228_psi2(const j228& p) {
   const f28 cx = f28_c(PSI2_X28), cy = f28_c(PSI2_Y28);
   return {{f28_mul(p.x.c0, cx), f28_mul(p.x.c1, cx)}, {f28_mul(p.y.c0, cy), f28_mul(p.y.c1, cy)}, p.z, p.inf};
 }
-DH_DEV j228 j228_mul_uabs(const j228& p) {  // [|u|] P, Jacobian base
+// the doubling runs of [|u|] between |u|'s set bits below the top one (62, 60, 57, 48, 16: 1, 2, 3, 9, 32, 16)
+DH_DEV int uabs_run(int r) { return r == 0 ? 1 : r == 1 ? 2 : r == 2 ? 3 : r == 3 ? 9 : r == 4 ? 32 : 16; }
+DH_DEV j228 j228_mul_uabs(const j228& p) {  // [|u|] P, Jacobian base; doublings in runs (g2_mul_uabs_ld)
   j228 acc = p;
 #pragma unroll 1
-  for (int b = 62; b >= 0; b--) {
-    acc = j228_dbl(acc);
-    if ((cst::U_ABS >> b) & 1) acc = j228_add<true>(acc, p);
+  for (int r = 0; r < 6; r++) {
+    const int k = uabs_run(r);
+#pragma unroll 1
+    for (int i = 0; i < k; i++) acc = j228_dbl(acc);
+    if (r < 5) acc = j228_add<true>(acc, p);
   }
   return acc;
 }
@@ -243,13 +247,17 @@ DH_DEV jac<fp2> g2_clear28(const jac<fp2>& q) {
 // [|u|] P on the lazy form; EXACT = false takes the mixed additions without their exceptional-case tests (the MSM's
 // fast formulas): an exceptional case (acc = +-P, or a 2-torsion doubling) leaves Z = 0 mod p, which every later step
 // keeps, so a poisoned result (Z = 0 without the infinity flag) is recomputed with the exact formulas
+// The 63 doublings run as the six runs between |u|'s set bits (uabs_run), each an inner loop with the mixed addition
+// after it, so the doublings' loop carries none of the addition's live values.
 template <bool EXACT, class Q>
 DH_DEV j228 g2_mul_uabs_ld(Q q) {
   j228 acc{q(0), q(1), f2_one(), false};
 #pragma unroll 1
-  for (int b = 62; b >= 0; b--) {
-    acc = j228_dbl<true>(acc);
-    if ((cst::U_ABS >> b) & 1) acc = j228_madd_ld<EXACT, true>(acc, q);
+  for (int r = 0; r < 6; r++) {
+    const int k = uabs_run(r);
+#pragma unroll 1
+    for (int i = 0; i < k; i++) acc = j228_dbl<true>(acc);
+    if (r < 5) acc = j228_madd_ld<EXACT, true>(acc, q);
   }
   return acc;
 }
