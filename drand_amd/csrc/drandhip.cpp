@@ -1069,11 +1069,12 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   HIP_TRY(w->r_den.ensure(n_rounds * (size_t)t * 32));
   HIP_TRY(w->r_lam.ensure(n_rounds * (size_t)t * 48 * 4));  // k_recover.hip LAM_WORDS per term
   HIP_TRY(w->r_rok.ensure(n_rounds));
+  HIP_TRY(w->r_lamset.ensure(n_rounds * 4));
   HIP_TRY(w->r_sig.ensure(n_rounds * jw * 4));
   HIP_TRY(T.run("k_select_lagrange", [&] {
     return dh::launch_select_lagrange(w->r_off.as<uint32_t>(), w->r_ok.as<uint8_t>(), w->r_pidx.as<uint32_t>(), t, n_rounds,
                                       w->r_sel.as<uint32_t>(), w->r_key.as<uint32_t>(), w->r_den.as<uint32_t>(),
-                                      w->r_lam.as<uint32_t>(), w->r_rok.as<uint8_t>(), st);
+                                      w->r_lam.as<uint32_t>(), w->r_lamset.as<uint32_t>(), w->r_rok.as<uint8_t>(), st);
   }));
   // 13. interpolation on the device
   if (g2) {  // the partials' points in the 28-bit form, and their width-4 NAF tables, once per valid partial
@@ -1086,7 +1087,8 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   }
   HIP_TRY(w->r_ltmp.ensure(dh::lagrange_tmp_bytes(g2)));
   HIP_TRY(T.run("k_lagrange", [&] {
-    return dh::launch_lagrange(g2, w->r_sel.as<uint32_t>(), w->r_lam.as<uint32_t>(), nullptr, w->r_rok.as<uint8_t>(), t,
+    return dh::launch_lagrange(g2, w->r_sel.as<uint32_t>(), w->r_lam.as<uint32_t>(), w->r_lamset.as<uint32_t>(),
+                               w->r_rok.as<uint8_t>(), t,
                                n_rounds, w->r_paff.as<uint32_t>(), g2 ? w->r_tbl.as<uint32_t>() : nullptr,
                                w->r_sig.as<uint32_t>(), w->r_ltmp.as<uint32_t>(), st);
   }));

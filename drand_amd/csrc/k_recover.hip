@@ -122,13 +122,13 @@ __global__ __launch_bounds__(256) void k_ok_from_status(const uint8_t* __restric
 // Recover's selection and Lagrange basis per round, one lane per round (kyber v1.1.18 tbls.Recover +
 // share.RecoverCommit / xyCommit, restated in oracle/bls_oracle.c or_recover): the first t valid partials in arrival
 // order (Recover stops at t), sorted by share index (stable), duplicate indices dropped; fewer than t distinct ->
-// not recovered. Then lambda_k = prod_{m != k} x_m / (x_m - x_k) over x = index + 1 in F_r (one batch inversion),
-// written for k_lagrange as NAF digit masks (G1) and width-4 NAF nibbles (G2). sel/key: t words per round; den: 8 t words
-// per round (scratch); lam: LAM_WORDS (48) t words per round: per term pos mask (8), neg mask (8), nibbles (32).
+// not recovered. Then (k_lambda) lambda_k = prod_{m != k} x_m / (x_m - x_k) over x = index + 1 in F_r (one batch
+// inversion), written for k_lagrange as NAF digit masks (G1) and width-4 NAF nibbles (G2). sel/key: t words per round;
+// den: 8 t words per round (scratch); lam: LAM_WORDS (48) t words per round: per term pos mask (8), neg mask (8),
+// nibbles (32).
 __global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restrict__ off, const uint8_t* __restrict__ ok,
                                                         const uint32_t* __restrict__ share_idx, int t, size_t n_rounds,
                                                         uint32_t* __restrict__ sel, uint32_t* __restrict__ key,
-                                                        uint32_t* __restrict__ den, uint32_t* __restrict__ lam,
                                                         uint8_t* __restrict__ rok) {
   const size_t j = gtid();
   if (j >= n_rounds) return;
@@ -155,11 +155,27 @@ __global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restri
     S[nd] = S[a];
     nd++;
   }
-  if (nd < t) {
-    rok[j] = 0;
-    return;
+  rok[j] = nd < t ? 0 : 1;
+}
+
+// lambda rows per recovered round; a round whose selected indices equal round 0's (the usual case: the same nodes
+// answer every round) points at round 0's rows (lam_set[j] = 0) instead of recomputing the same basis, otherwise
+// lam_set[j] = j. lam_set is what k_lagrange reads.
+__global__ __launch_bounds__(64) void k_lambda(const uint32_t* __restrict__ key, const uint8_t* __restrict__ rok, int t,
+                                               size_t n_rounds, uint32_t* __restrict__ den, uint32_t* __restrict__ lam,
+                                               uint32_t* __restrict__ lam_set) {
+  const size_t j = gtid();
+  if (j >= n_rounds || !rok[j]) return;
+  const uint32_t* K = key + j * (size_t)t;
+  if (j > 0 && rok[0]) {
+    bool same = true;
+    for (int k = 0; k < t && same; k++) same = K[k] == key[k];
+    if (same) {
+      lam_set[j] = 0;
+      return;
+    }
   }
-  rok[j] = 1;
+  lam_set[j] = (uint32_t)j;
   uint32_t* D = den + j * (size_t)t * 8;
   uint32_t* L = lam + j * (size_t)t * LAM_WORDS;
   // pass 1: numerators (into lam's second half), denominators (scratch), prefix products (into lam's first half)
@@ -240,13 +256,15 @@ __global__ __launch_bounds__(64) void k_partial_leaf(const uint32_t* __restrict_
 // lam: per term the NAF masks of lambda (16 words); row set lam_set[j], or the round's own rows when lam_set is null.
 // LG_LANES lanes per round, each running Straus (shared doublings) over every LG_LANES-th term of the
 // interpolation sum sum_k lambda_k sigma_k; the partial sums meet in LDS and one lane of the round adds them. One
-// lane per round left most of the chip idle at 10^4-10^5 rounds and ran 33 terms x 127 additions serially; four lanes
-// cut the per-round latency ~3.8x for ~6% more doublings. A workgroup is LG_LANES waves over the same 64 rounds, wave q
+// lane per round left most of the chip idle at 10^4-10^5 rounds and ran 33 terms x 127 additions serially. With the
+// width-4 NAF the 256 doublings per lane are a quarter of the chain's products, so r04 measured 2 lanes against 4 on
+// one box: k_lagrange 119.7 -> 103.2 ms per 100k rounds (the last partial wave of workgroups sliced either way;
+// profiles/r04/config_recover_lanes*). A workgroup is LG_LANES waves over the same 64 rounds, wave q
 // running term lane q of each: rounds that selected the same signers (the usual case: the same nodes answer every
 // round) have the same lambdas, so all 64 lanes of a wave take the same digits and branches. r03 put the LG_LANES
 // lanes of a round side by side in ONE wave, whose lanes then followed LG_LANES different digit patterns and ran
 // every addition step up to LG_LANES times, diverged.
-constexpr int LG_LANES = 4, LG_MAXK = 9;  // terms per lane and pass (t <= 36: one pass)
+constexpr int LG_LANES = 2, LG_MAXK = 17;  // terms per lane and pass (t <= 34: one pass)
 // G2: the chain on the lazily reduced 28-bit form (fp2_28.hpp) over width-4 NAF digits and each partial's table of
 // P, 3P, 5P, 7P (1/5 of the positions take an addition instead of 1/3), with the MSM's fast mixed additions (no
 // exceptional-case tests); a chain that met an exceptional case ends with Z = 0 mod p and runs again with the exact
@@ -556,10 +574,12 @@ hipError_t launch_ok_from_status(const uint8_t* status, size_t np, uint8_t* ok, 
 }
 
 hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const uint32_t* share_idx, int t, size_t n_rounds,
-                                  uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint8_t* rok, hipStream_t st) {
+                                  uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint32_t* lam_set, uint8_t* rok,
+                                  hipStream_t st) {
   if (!n_rounds) return hipSuccess;
   hipLaunchKernelGGL(k_select_lagrange, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, off, ok, share_idx, t, n_rounds, sel, key,
-                     den, lam, rok);
+                     rok);
+  hipLaunchKernelGGL(k_lambda, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, key, rok, t, n_rounds, den, lam, lam_set);
   return hipGetLastError();
 }
 
@@ -572,14 +592,16 @@ static int cu_count() {
   }();
   return n;
 }
-size_t lagrange_tmp_bytes(int sig_g2) { return (size_t)cu_count() * 64 * (sig_g2 ? 72 : 36) * 4; }
+// workgroups resident at once: LG_LANES waves each at one wave per SIMD (the kernel holds 512 registers), 4 SIMDs per CU
+static size_t lagrange_slots() { return (size_t)cu_count() * (4 / LG_LANES); }
+size_t lagrange_tmp_bytes(int sig_g2) { return lagrange_slots() * 64 * (sig_g2 ? 72 : 36) * 4; }
 
 template <class F>
 static void lagrange_grid(const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok, int t,
                           size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, uint32_t* out, uint32_t* tmp,
                           hipStream_t st) {
-  // one workgroup (LG_LANES waves) per CU at a time: blocks beyond the last full wave of CUs are sliced (k_lagrange)
-  const size_t nb = nblk(n_rounds, 64), ncu = (size_t)cu_count();
+  // blocks beyond the last full wave of resident workgroups are sliced (k_lagrange)
+  const size_t nb = nblk(n_rounds, 64), ncu = lagrange_slots();
   size_t full = nb, rem = 0, S = 1;
   const size_t max_s = (size_t)(t + LG_LANES - 1) / LG_LANES;
   if (tmp && nb > ncu && nb % ncu && nb % ncu <= ncu / 2 && max_s > 1) {

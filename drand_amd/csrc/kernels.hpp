@@ -144,9 +144,11 @@ hipError_t launch_partial_meta(const uint32_t* off, size_t n_rounds, const uint3
                                uint8_t* status, hipStream_t st);
 hipError_t launch_clamp_group(const uint32_t* share_idx, size_t np, uint32_t hi, uint32_t* grp, hipStream_t st);
 hipError_t launch_ok_from_status(const uint8_t* status, size_t np, uint8_t* ok, hipStream_t st);
-// per round: Recover's selection + Lagrange coefficients (sel/key: t words, den: 8t words, lam: 48t words per round)
+// per round: Recover's selection + Lagrange coefficients (sel/key: t words, den: 8t words, lam: 48t words per round);
+// lam_set[j] = the round whose lambda rows round j uses (0 when its selected indices equal round 0's, else j)
 hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const uint32_t* share_idx, int t, size_t n_rounds,
-                                  uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint8_t* rok, hipStream_t st);
+                                  uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint32_t* lam_set, uint8_t* rok,
+                                  hipStream_t st);
 // tbl (G2): per valid partial (ok) P, 3P, 5P, 7P affine 28-bit (256 words each) from the partials' affine points
 // (12 x 32-bit AOS); zs: wnaf_table_scratch_bytes(n) of scratch (the batched inversion's Z's); unused for G1
 hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, uint32_t* tbl, uint32_t* zs,

@@ -229,8 +229,9 @@ def test_recover_large_batch_sliced_and_chunked(dh, oracle):
     """A Recover batch big enough for the paths a 160-round test never takes: 18,944 rounds are 296 blocks of 64, so
     k_lagrange's last 40 blocks (past 256 CUs) run sliced over 6 workgroups each and are summed by k_lagrange_sum;
     551k partial records cross to the device in two chunks overlapped with their decoding. Rounds carry t + 1 partials
-    of a random signer subset (a different Lagrange basis per round), every 7th round one invalid partial in front
-    (still t valid), every 101st two more (fewer than t valid: not recovered). Recovered = the group signature [f(0)] H(m);
+    of a random signer subset (every second round the signers of round 0, whose Lagrange rows it then shares, the others a basis of
+    their own), every 7th round one invalid partial in front (still t valid, a different basis), every 101st two more
+    (fewer than t valid: not recovered). Recovered = the group signature [f(0)] H(m);
     a few rounds against the oracle."""
     s = dh.scheme_from_name("pedersen-bls-unchained")
     n, t, nr = 30, 28, 18944
@@ -239,13 +240,14 @@ def test_recover_large_batch_sliced_and_chunked(dh, oracle):
     shares = np.stack([s.sign_beacons(_share(coeffs, i), rounds) for i in range(n)])  # (n, nr, 96)
     rng = np.random.default_rng(55)
     ids = np.argsort(rng.random((nr, n)), axis=1)[:, :t + 1]
+    ids[::2] = ids[0]  # every second round the signers (and arrival order) of round 0: their lambda rows are round 0's
     raw = np.zeros((nr, t + 1, 98), dtype=np.uint8)
     raw[:, :, 0] = (ids >> 8).astype(np.uint8)
     raw[:, :, 1] = (ids & 0xff).astype(np.uint8)
     raw[:, :, 2:] = shares[ids, np.arange(nr)[:, None]]
-    bad1 = np.arange(0, nr, 7)
+    bad1 = np.arange(3, nr, 7)
     raw[bad1, 0, 2 + 40] ^= 0x08
-    bad2 = np.arange(0, nr, 101)
+    bad2 = np.arange(5, nr, 101)
     raw[bad2, 1, 2:] = shares[ids[bad2, 1], (bad2 + 1) % nr]  # another round's signature
     raw[bad2, 2, 2 + 60] ^= 0x01
     raw = raw.reshape(nr * (t + 1), 98)
@@ -257,7 +259,7 @@ def test_recover_large_batch_sliced_and_chunked(dh, oracle):
     assert np.array_equal(ok, want_ok)
     group = s.sign_beacons(coeffs[0].to_bytes(32, "big"), rounds)
     assert np.array_equal(sigs[ok], group[ok])
-    for j in [1, 7, 101, nr - 1]:
+    for j in [0, 1, 2, 10, 3, 5, nr - 1]:
         parts = [raw[j * (t + 1) + k].tobytes() for k in range(t + 1)]
         got = oracle.recover(s.name, commits, t, n, msgs[j].tobytes(), parts)
         assert (got is not None) == bool(ok[j]) and (got is None or got == sigs[j].tobytes()), j
