@@ -112,7 +112,7 @@ struct worker {
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
-      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_zs, r_tbl, r_rstat, r_ltmp;
+      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_zs, r_tbl, r_rstat, r_ltmp, r_own;
   std::vector<uint8_t> h_verdict;
   // Recover: the (scheme, t, n_nodes, commits) whose decoded commits and public shares r_caff / r_shares hold
   std::vector<uint8_t> r_pub_key;
@@ -130,7 +130,7 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_zs, &r_tbl, &r_rstat, &r_ltmp, &node_sum, &node_res};
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_zs, &r_tbl, &r_rstat, &r_ltmp, &r_own, &node_sum, &node_res};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
     if (tail) (void)hipStreamDestroy(tail);
@@ -1067,21 +1067,32 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   HIP_TRY(w->r_sel.ensure(n_rounds * (size_t)t * 4));
   HIP_TRY(w->r_key.ensure(n_rounds * (size_t)t * 4));
   HIP_TRY(w->r_den.ensure(n_rounds * (size_t)t * 32));
-  HIP_TRY(w->r_lam.ensure(n_rounds * (size_t)t * 48 * 4));  // k_recover.hip LAM_WORDS per term
+  HIP_TRY(w->r_lam.ensure(n_rounds * (size_t)t * dh::lam_words() * 4));
   HIP_TRY(w->r_rok.ensure(n_rounds));
   HIP_TRY(w->r_lamset.ensure(n_rounds * 4));
+  HIP_TRY(w->r_own.ensure(4));
   HIP_TRY(w->r_sig.ensure(n_rounds * jw * 4));
   HIP_TRY(T.run("k_select_lagrange", [&] {
     return dh::launch_select_lagrange(w->r_off.as<uint32_t>(), w->r_ok.as<uint8_t>(), w->r_pidx.as<uint32_t>(), t, n_rounds,
                                       w->r_sel.as<uint32_t>(), w->r_key.as<uint32_t>(), w->r_den.as<uint32_t>(),
-                                      w->r_lam.as<uint32_t>(), w->r_lamset.as<uint32_t>(), w->r_rok.as<uint8_t>(), st);
+                                      w->r_lam.as<uint32_t>(), w->r_lamset.as<uint32_t>(), w->r_rok.as<uint8_t>(),
+                                      w->r_own.as<uint32_t>(), st);
   }));
+  // tables of 8 odd multiples when some round has a Lagrange basis of its own (its wave then runs the regular windows
+  // in k_lagrange), else of 4 for the width-4 NAF: one word back from the device
+  int entries = 4;
+  if (g2) {
+    uint32_t own = 0;
+    HIP_TRY(hipMemcpyAsync(&own, w->r_own.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (own) entries = 8;
+  }
   // 13. interpolation on the device
   if (g2) {  // the partials' points in the 28-bit form, and their width-4 NAF tables, once per valid partial
-    HIP_TRY(w->r_zs.ensure(dh::wnaf_table_scratch_bytes(np) + 256));
-    HIP_TRY(w->r_tbl.ensure(np * 256 * 4 + 1024));
+    HIP_TRY(w->r_zs.ensure(dh::wnaf_table_scratch_bytes(np, entries) + 256));
+    HIP_TRY(w->r_tbl.ensure(np * (size_t)entries * 64 * 4 + 1024));
     HIP_TRY(T.run("k_wnaf_table", [&] {
-      return dh::launch_wnaf_table_g2(w->r_paff.as<uint32_t>(), w->r_ok.as<uint8_t>(), np, w->r_tbl.as<uint32_t>(),
+      return dh::launch_wnaf_table_g2(w->r_paff.as<uint32_t>(), w->r_ok.as<uint8_t>(), np, entries, w->r_tbl.as<uint32_t>(),
                                       w->r_zs.as<uint32_t>(), st);
     }));
   }
@@ -1089,7 +1100,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   HIP_TRY(T.run("k_lagrange", [&] {
     return dh::launch_lagrange(g2, w->r_sel.as<uint32_t>(), w->r_lam.as<uint32_t>(), w->r_lamset.as<uint32_t>(),
                                w->r_rok.as<uint8_t>(), t,
-                               n_rounds, w->r_paff.as<uint32_t>(), g2 ? w->r_tbl.as<uint32_t>() : nullptr,
+                               n_rounds, w->r_paff.as<uint32_t>(), g2 ? w->r_tbl.as<uint32_t>() : nullptr, entries,
                                w->r_sig.as<uint32_t>(), w->r_ltmp.as<uint32_t>(), st);
   }));
   std::vector<uint8_t> rok(n_rounds, 0);

@@ -151,6 +151,50 @@ DH_DEV void fr_wnaf4(const uint32_t w[8], uint32_t* nib) {
   }
 }
 
+// Regular signed 4-bit windows of a scalar 0 < w < r (little-endian words): 64 digits, every one odd and nonzero,
+// sum d_i 16^i = w, so a Straus chain adds at every window with no digit-dependent branch (k_lagrange's path for waves
+// whose rounds do not share one Lagrange basis). An even w is recoded as r - w (odd) with every digit negated
+// ([-(r - w)] P = [w] P on the order-r subgroup). Digit i in nibble i (word i / 8, bits 4 (i % 8)): (|d| - 1) / 2 in
+// bits 0-2 (table entry P, 3P, ..., 15P), bit 3 the sign. Steps: d = (k mod 32) - 16 (odd, |d| <= 15), k = (k - d) / 16
+// stays odd; after 63 steps k <= 2^255 / 2^252 + 16 / 15 is the last digit (1 .. 9).
+DH_DEV void fr_reg4(const uint32_t w[8], uint32_t* nib) {
+  uint32_t k[8];
+  const bool flip = !(w[0] & 1);
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = flip ? __builtin_subc(FR_MOD[i], w[i], br, &br) : w[i];
+  uint32_t acc = 0;
+#pragma unroll 1
+  for (int i = 0; i < 64; i++) {
+    int d;
+    if (i < 63) {
+      d = (int)(k[0] & 31) - 16;
+      // k -= d (k - d = 16 mod 32), then k >>= 4
+      if (d < 0) {
+        unsigned c = (unsigned)(-d);
+#pragma unroll
+        for (int m = 0; m < 8; m++) k[m] = __builtin_addc(k[m], 0u, c, &c);
+      } else {
+        unsigned b = (unsigned)d;
+#pragma unroll
+        for (int m = 0; m < 8; m++) k[m] = __builtin_subc(k[m], 0u, b, &b);
+      }
+#pragma unroll
+      for (int m = 0; m < 7; m++) k[m] = (k[m] >> 4) | (k[m + 1] << 28);
+      k[7] >>= 4;
+    } else {
+      d = (int)k[0];
+    }
+    if (flip) d = -d;
+    const uint32_t v = (uint32_t)((d < 0 ? -d : d) - 1) / 2 | (d < 0 ? 8u : 0u);
+    acc |= v << (4 * (i & 7));
+    if ((i & 7) == 7) {
+      nib[i >> 3] = acc;
+      acc = 0;
+    }
+  }
+}
+
 DH_DEV void fr_naf_masks(const uint32_t w[8], uint32_t* pos, uint32_t* neg) {
   uint32_t k[9];
 #pragma unroll

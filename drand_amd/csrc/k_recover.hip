@@ -17,7 +17,8 @@
 
 namespace dh {
 
-constexpr int LAM_WORDS = 48;  // per Lagrange term: NAF pos mask (8 words), neg mask (8), width-4 NAF nibbles (32)
+// per Lagrange term: NAF pos mask (8 words), neg mask (8), width-4 NAF nibbles (32), regular 4-bit window digits (32)
+constexpr int LAM_WORDS = 80;
 
 __global__ void k_repack_partials(const uint8_t* __restrict__ raw, size_t n, int sig_len, uint8_t* __restrict__ sigs,
                                   uint32_t* __restrict__ idx) {
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restri
 // lam_set[j] = j. lam_set is what k_lagrange reads.
 __global__ __launch_bounds__(64) void k_lambda(const uint32_t* __restrict__ key, const uint8_t* __restrict__ rok, int t,
                                                size_t n_rounds, uint32_t* __restrict__ den, uint32_t* __restrict__ lam,
-                                               uint32_t* __restrict__ lam_set) {
+                                               uint32_t* __restrict__ lam_set, uint32_t* __restrict__ own) {
   const size_t j = gtid();
   if (j >= n_rounds || !rok[j]) return;
   const uint32_t* K = key + j * (size_t)t;
@@ -176,6 +177,7 @@ __global__ __launch_bounds__(64) void k_lambda(const uint32_t* __restrict__ key,
     }
   }
   lam_set[j] = (uint32_t)j;
+  if (j > 0) atomicAdd(own, 1u);
   uint32_t* D = den + j * (size_t)t * 8;
   uint32_t* L = lam + j * (size_t)t * LAM_WORDS;
   // pass 1: numerators (into lam's second half), denominators (scratch), prefix products (into lam's first half)
@@ -215,6 +217,7 @@ __global__ __launch_bounds__(64) void k_lambda(const uint32_t* __restrict__ key,
       L[LAM_WORDS * k + 8 + w] = neg[w];
     }
     fr_wnaf4(words, L + LAM_WORDS * k + 16);
+    fr_reg4(words, L + LAM_WORDS * k + 48);
   }
 }
 
@@ -291,95 +294,96 @@ DH_DEV void st_f28w(uint32_t* p, const f28& a) {
   for (int i = 0; i < 4; i++)
     q[i] = make_uint4(a.l[4 * i], a.l[4 * i + 1], 4 * i + 2 < 14 ? a.l[4 * i + 2] : 0u, 4 * i + 3 < 14 ? a.l[4 * i + 3] : 0u);
 }
-// G2 width-4 NAF table per valid partial: P, 3P, 5P, 7P affine in the 28-bit form (WT x 64 words). The Jacobian Z's
-// of 3P, 5P, 7P are inverted with Montgomery's trick over TB_K partials per lane (one variable-time Fp2 inversion per
-// lane instead of per partial: r04d spent 30.6 ms on 3.3M tables with one inversion each); the lane parks each
-// partial's three Z's and the running product before it in zs (128 words per partial) and walks back after the
-// inversion. The partials reaching k_lagrange decoded to subgroup points, so 2P, 3P, 5P, 7P are finite and distinct
-// from the points added to them: the exact formulas only guard the table of a partial that is never selected.
-constexpr int WT = 4, TBL_WORDS = WT * A28_WORDS, TB_K = 8, ZS_WORDS = 128;
+// G2 table per valid partial: the odd multiples P, 3P, ..., (2 NE - 1) P affine in the 28-bit form (NE x 64 words):
+// NE = 4 for the width-4 NAF chains (digits up to 7), NE = 8 when some wave's rounds do not share one Lagrange basis and
+// run the regular 4-bit windows (digits up to 15). The Jacobian Z's of all the lane's entries (TB_K partials x NE - 1)
+// share one variable-time Fp2 inversion by Montgomery's trick (r04d spent 30.6 ms on 3.3M tables with one inversion
+// per partial): each Z and the product of the lane's Z's before it are parked in zs, X and Y in their table slots,
+// and the walk back after the inversion turns each entry affine. The partials reaching k_lagrange decoded to subgroup
+// points, so the multiples are finite and distinct from the points added to them: the exact formulas only guard the
+// table of a partial that is never selected.
+constexpr int TB_K = 8;
 DH_DEV void st_f228w(uint32_t* p, const f228& a) {
   st_f28w(p, a.c0);
   st_f28w(p + 16, a.c1);
 }
 DH_DEV f228 ld_f228w(const uint32_t* p) { return f228{ld_f28w(p), ld_f28w(p + 16)}; }
+template <int NE>
 __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restrict__ paff, const uint8_t* __restrict__ ok,
                                                        size_t n, uint32_t* __restrict__ tbl, uint32_t* __restrict__ zs) {
+  constexpr size_t TW = (size_t)NE * A28_WORDS, ZW = (size_t)(NE - 1) * 64;  // words per partial: table, scratch
   const size_t nth = (n + TB_K - 1) / TB_K;
   const size_t t = gtid();
   if (t >= nth) return;
   f228 pre = f2_one();
+  bool any = false;
   uint32_t valid = 0;  // bit k: the lane's k-th partial is valid
 #pragma unroll 1
   for (int k = 0; k < TB_K; k++) {
     const size_t e = t + (size_t)k * nth;  // lanes of a wave take consecutive partials
     if (e >= n || !ok[e]) continue;
+    valid |= 1u << k;
     const aff<fp2> a = ld_aff_aos<fp2>(paff, e);
     const f228 px{f28_from_fp(a.x.c0), f28_from_fp(a.x.c1)}, py{f28_from_fp(a.y.c0), f28_from_fp(a.y.c1)};
-    uint32_t* o = tbl + (size_t)TBL_WORDS * e;
-    uint32_t* z = zs + (size_t)ZS_WORDS * e;
+    uint32_t* o = tbl + TW * e;
+    uint32_t* z = zs + ZW * e;
     st_f228w(o, px);
     st_f228w(o + 32, py);
-    // 3P, 5P, 7P: X, Y parked in their table slots, Z's in zs, until the inversion
     const j228 two = j228_dbl(j228{px, py, f2_one(), false});
     j228 m = j228_madd<true>(two, px, py);  // 3P
-    f228 zp = f2_one();
 #pragma unroll 1
-    for (int j = 0; j < 3; j++) {
-      if (j) m = j228_add<true>(m, two);  // 5P, 7P
-      uint32_t* sl = o + A28_WORDS * (j + 1);
+    for (int j = 1; j < NE; j++) {
+      if (j > 1) m = j228_add<true>(m, two);  // (2j + 1) P
+      uint32_t* sl = o + A28_WORDS * j;
       st_f228w(sl, m.x);
       st_f228w(sl + 32, m.y);
-      st_f228w(z + 32 * j, m.z);
-      zp = j ? f2_red(f2_mul(zp, m.z)) : m.z;
+      st_f228w(z + 64 * (j - 1), m.z);
+      if (any) st_f228w(z + 64 * (j - 1) + 32, pre);  // the product of the lane's Z's before this one
+      pre = any ? f2_red(f2_mul(pre, m.z)) : m.z;
+      any = true;
     }
-    if (valid) st_f228w(z + 96, pre);  // the product of the lane's earlier Z's
-    pre = valid ? f2_red(f2_mul(pre, zp)) : zp;
-    valid |= 1u << k;
   }
-  if (!valid) return;
+  if (!any) return;
   f228 inv = f2_from_fp2(fp2_inv_vt(f2_to_fp2(pre)));  // 1 / (product of every Z of the lane)
 #pragma unroll 1
   for (int k = TB_K - 1; k >= 0; k--) {
     if (!(valid >> k & 1)) continue;
     const size_t e = t + (size_t)k * nth;
-    const uint32_t* z = zs + (size_t)ZS_WORDS * e;
-    const f228 z0 = ld_f228w(z), z1 = ld_f228w(z + 32), z2 = ld_f228w(z + 64);
-    const f228 z01 = f2_red(f2_mul(z0, z1));
-    // this partial's 1 / (z0 z1 z2): inv times the product of the Z's before it (the lane's first: inv itself);
-    // inv then becomes 1 / that product
-    f228 ip = inv;
-    if (valid & ((1u << k) - 1)) {
-      ip = f2_red(f2_mul(inv, ld_f228w(z + 96)));
-      inv = f2_red(f2_mul(inv, f2_red(f2_mul(z01, z2))));
-    }
-    f228 zi[3];
-    zi[2] = f2_red(f2_mul(ip, z01));
-    const f228 i01 = f2_red(f2_mul(ip, z2));  // 1 / (z0 z1)
-    zi[1] = f2_red(f2_mul(i01, z0));
-    zi[0] = f2_red(f2_mul(i01, z1));
-    uint32_t* o = tbl + (size_t)TBL_WORDS * e;
+    const uint32_t* z = zs + ZW * e;
+    uint32_t* o = tbl + TW * e;
+    const bool earlier = (valid & ((1u << k) - 1)) != 0;  // a valid partial before this one in the lane
 #pragma unroll 1
-    for (int j = 0; j < 3; j++) {
-      uint32_t* sl = o + A28_WORDS * (j + 1);
-      const f228 z2j = f2_red(f2_sqr<2>(zi[j]));
-      st_f228w(sl, f2_red(f2_mul(ld_f228w(sl), z2j)));
-      st_f228w(sl + 32, f2_red(f2_mul(ld_f228w(sl + 32), f2_red(f2_mul(z2j, zi[j])))));
+    for (int j = NE - 1; j >= 1; j--) {
+      // the lane's first Z: inv is its inverse; otherwise inv * (product before it), and inv moves past it
+      const bool later = earlier || j > 1;
+      f228 zi = inv;
+      if (later) {
+        zi = f2_red(f2_mul(inv, ld_f228w(z + 64 * (j - 1) + 32)));
+        inv = f2_red(f2_mul(inv, ld_f228w(z + 64 * (j - 1))));
+      }
+      uint32_t* sl = o + A28_WORDS * j;
+      const f228 z2 = f2_red(f2_sqr<2>(zi));
+      st_f228w(sl, f2_red(f2_mul(ld_f228w(sl), z2)));
+      st_f228w(sl + 32, f2_red(f2_mul(ld_f228w(sl + 32), f2_red(f2_mul(z2, zi)))));
     }
   }
 }
-hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, uint32_t* tbl, uint32_t* zs,
+hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, int entries, uint32_t* tbl, uint32_t* zs,
                                 hipStream_t st) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_wnaf_table_g2, dim3(nblk((n + TB_K - 1) / TB_K, 256)), dim3(256), 0, st, paff, ok, n, tbl, zs);
+  if (entries == 8)
+    hipLaunchKernelGGL(k_wnaf_table_g2<8>, dim3(nblk((n + TB_K - 1) / TB_K, 256)), dim3(256), 0, st, paff, ok, n, tbl, zs);
+  else
+    hipLaunchKernelGGL(k_wnaf_table_g2<4>, dim3(nblk((n + TB_K - 1) / TB_K, 256)), dim3(256), 0, st, paff, ok, n, tbl, zs);
   return hipGetLastError();
 }
-size_t wnaf_table_scratch_bytes(size_t n) { return n * ZS_WORDS * 4; }
+size_t wnaf_table_scratch_bytes(size_t n, int entries) { return n * (size_t)(entries - 1) * 64 * 4; }
+size_t lam_words() { return LAM_WORDS; }
 
 // the width-4 NAF Straus chain of one lane's terms over their tables (nibble words of the current 8 positions in nw)
 template <bool EXACT>
 DH_DEV j228 lagrange_wnaf28(const uint32_t* __restrict__ L, int q, int nl, int c0, int nc, const uint32_t* __restrict__ tbl,
-                            const uint32_t* idx, uint32_t* nw) {
+                            uint32_t tw, const uint32_t* idx, uint32_t* nw) {
   j228 acc = j228_inf();
 #pragma unroll 1
   for (int b = 255; b >= 0; b--) {
@@ -390,12 +394,42 @@ DH_DEV j228 lagrange_wnaf28(const uint32_t* __restrict__ L, int q, int nl, int c
     for (int i = 0; i < nc; i++) {
       const uint32_t v = (nw[i] >> (4 * (b & 7))) & 15;
       if (v) {
-        const uint32_t* pt = tbl + (size_t)TBL_WORDS * idx[i] + A28_WORDS * ((v & 7) - 1);
+        const uint32_t* pt = tbl + (size_t)tw * idx[i] + A28_WORDS * ((v & 7) - 1);
         const f228 x{ld_f28w(pt), ld_f28w(pt + 16)};
         f228 y{ld_f28w(pt + 32), ld_f28w(pt + 48)};
         if (v & 8) y = f2_neg3(y);
         acc = j228_madd<EXACT>(acc, x, y);
       }
+    }
+  }
+  return acc;
+}
+
+// the regular 4-bit window chain (fr_reg4 digits, every one odd and nonzero) of one lane's terms over their 8-entry
+// tables: four doublings and one mixed addition per term at each of the 64 windows, with no digit-dependent branch —
+// the path of a wave whose rounds use different Lagrange bases (random signer subsets), where the width-4 NAF's
+// per-lane digits left the wave running nearly every position's addition for some lane (k_lagrange 540-590 ms per
+// 100k random-subset rounds against 103-120 ms coherent, profiles/r04/config_recover_random_*)
+template <bool EXACT>
+DH_DEV j228 lagrange_reg28(const uint32_t* __restrict__ L, int q, int nl, int c0, int nc, const uint32_t* __restrict__ tbl,
+                           uint32_t tw, const uint32_t* idx, uint32_t* nw) {
+  j228 acc = j228_inf();
+#pragma unroll 1
+  for (int wi = 63; wi >= 0; wi--) {
+    if ((wi & 7) == 7)
+      for (int i = 0; i < nc; i++) nw[i] = L[(size_t)(q + nl * (c0 + i)) * LAM_WORDS + 48 + (wi >> 3)];
+    if (!acc.inf) {
+#pragma unroll 1
+      for (int d = 0; d < 4; d++) acc = j228_dbl(acc);
+    }
+#pragma unroll 1
+    for (int i = 0; i < nc; i++) {
+      const uint32_t v = (nw[i] >> (4 * (wi & 7))) & 15;
+      const uint32_t* pt = tbl + (size_t)tw * idx[i] + A28_WORDS * (v & 7);
+      const f228 x{ld_f28w(pt), ld_f28w(pt + 16)};
+      f228 y{ld_f28w(pt + 32), ld_f28w(pt + 48)};
+      if (v & 8) y = f2_neg3(y);
+      acc = j228_madd<EXACT>(acc, x, y);
     }
   }
   return acc;
@@ -411,8 +445,9 @@ template <class F>
 __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __restrict__ sel, const uint32_t* __restrict__ lam,
                                                             const uint32_t* __restrict__ lam_set, const uint8_t* __restrict__ ok,
                                                             int t, size_t n_rounds, const uint32_t* __restrict__ sig_aff,
-                                                            const uint32_t* __restrict__ tbl, uint32_t* __restrict__ out,
-                                                            uint32_t full, uint32_t S, uint32_t* __restrict__ part_out) {
+                                                            const uint32_t* __restrict__ tbl, uint32_t tw, int reg,
+                                                            uint32_t* __restrict__ out, uint32_t full, uint32_t S,
+                                                            uint32_t* __restrict__ part_out) {
   constexpr int JW = sizeof(F) / 4 * 3;
   __shared__ uint32_t part[(LG_LANES - 1) * 64 * JW];  // the partial sums of waves 1 .. LG_LANES - 1
   __shared__ uint32_t idxS[64 * LG_LANES][LG_MAXK], lpS[64 * LG_LANES][LG_MAXK], lnS[64 * LG_LANES][LG_MAXK];
@@ -423,7 +458,14 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
   const int q = sl * LG_LANES + (int)(threadIdx.x / 64);  // term lane: wave-uniform
   const size_t j = blk * 64 + threadIdx.x % 64;
   jac<F> acc = jac_inf<F>();
-  if (j < n_rounds && ok[j]) {
+  // wave-uniform: do the wave's recovered rounds share one Lagrange basis (lam_set)? If not and the tables hold 8
+  // entries (reg), the regular windows instead of the width-4 NAF
+  const bool live = j < n_rounds && ok[j];
+  const uint32_t myset = live ? (lam_set ? lam_set[j] : (uint32_t)j) : 0xffffffffu;
+  const unsigned long long act = __ballot(live);
+  const uint32_t ref = __shfl(myset, act ? __ffsll((long long)act) - 1 : 0);
+  const bool regular = reg && !__all(!live || myset == ref);
+  if (live) {
     const uint32_t* L = lam + (lam_set ? (size_t)lam_set[j] : j) * t * LAM_WORDS;  // per term: NAF masks, wNAF nibbles
     const uint32_t* Sel = sel + j * (size_t)t;
     const int nt = q < t ? (t - q + nl - 1) / nl : 0;  // terms of this lane: k = q + nl i
@@ -437,8 +479,11 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
       if constexpr (sizeof(F) == sizeof(fp2)) {
         // width-4 NAF over the partials' tables; a chain that met an exceptional case (poisoned) runs again with
         // the exact formulas
-        j228 a28 = lagrange_wnaf28<false>(L, q, nl, c0, nc, tbl, idx, lp);
-        if (j228_poisoned(a28)) a28 = lagrange_wnaf28<true>(L, q, nl, c0, nc, tbl, idx, lp);
+        j228 a28 = regular ? lagrange_reg28<false>(L, q, nl, c0, nc, tbl, tw, idx, lp)
+                           : lagrange_wnaf28<false>(L, q, nl, c0, nc, tbl, tw, idx, lp);
+        if (j228_poisoned(a28))
+          a28 = regular ? lagrange_reg28<true>(L, q, nl, c0, nc, tbl, tw, idx, lp)
+                        : lagrange_wnaf28<true>(L, q, nl, c0, nc, tbl, tw, idx, lp);
         if (!a28.inf) acc = jac_add(acc, jac<F>{f2_to_fp2(a28.x), f2_to_fp2(a28.y), f2_to_fp2(a28.z)});
         continue;
       }
@@ -575,11 +620,13 @@ hipError_t launch_ok_from_status(const uint8_t* status, size_t np, uint8_t* ok, 
 
 hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const uint32_t* share_idx, int t, size_t n_rounds,
                                   uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint32_t* lam_set, uint8_t* rok,
-                                  hipStream_t st) {
+                                  uint32_t* own, hipStream_t st) {
   if (!n_rounds) return hipSuccess;
+  hipError_t e = hipMemsetAsync(own, 0, 4, st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_select_lagrange, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, off, ok, share_idx, t, n_rounds, sel, key,
                      rok);
-  hipLaunchKernelGGL(k_lambda, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, key, rok, t, n_rounds, den, lam, lam_set);
+  hipLaunchKernelGGL(k_lambda, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, key, rok, t, n_rounds, den, lam, lam_set, own);
   return hipGetLastError();
 }
 
@@ -598,8 +645,8 @@ size_t lagrange_tmp_bytes(int sig_g2) { return lagrange_slots() * 64 * (sig_g2 ?
 
 template <class F>
 static void lagrange_grid(const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok, int t,
-                          size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, uint32_t* out, uint32_t* tmp,
-                          hipStream_t st) {
+                          size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, int entries, uint32_t* out,
+                          uint32_t* tmp, hipStream_t st) {
   // blocks beyond the last full wave of resident workgroups are sliced (k_lagrange)
   const size_t nb = nblk(n_rounds, 64), ncu = lagrange_slots();
   size_t full = nb, rem = 0, S = 1;
@@ -610,18 +657,19 @@ static void lagrange_grid(const uint32_t* sel, const uint32_t* lam, const uint32
     S = std::min(max_s, ncu / rem);
   }
   hipLaunchKernelGGL(k_lagrange<F>, dim3(full + rem * S), dim3(64 * LG_LANES), 0, st, sel, lam, lam_set, ok, t, n_rounds,
-                     sig_aff, tbl, out, (uint32_t)full, (uint32_t)S, tmp);
+                     sig_aff, tbl, (uint32_t)(entries * A28_WORDS), entries == 8 ? 1 : 0, out, (uint32_t)full, (uint32_t)S,
+                     tmp);
   if (rem)
     hipLaunchKernelGGL(k_lagrange_sum<F>, dim3(nblk(n_rounds - full * 64, 64)), dim3(64), 0, st, tmp, (uint32_t)S, full * 64,
                        n_rounds, out);
 }
 
 hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
-                           int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, uint32_t* out,
+                           int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, int entries, uint32_t* out,
                            uint32_t* tmp, hipStream_t st) {
   if (!n_rounds) return hipSuccess;
-  if (sig_g2) lagrange_grid<fp2>(sel, lam, lam_set, ok, t, n_rounds, sig_aff, tbl, out, tmp, st);
-  else lagrange_grid<fp>(sel, lam, lam_set, ok, t, n_rounds, sig_aff, tbl, out, tmp, st);
+  if (sig_g2) lagrange_grid<fp2>(sel, lam, lam_set, ok, t, n_rounds, sig_aff, tbl, entries, out, tmp, st);
+  else lagrange_grid<fp>(sel, lam, lam_set, ok, t, n_rounds, sig_aff, tbl, entries, out, tmp, st);
   return hipGetLastError();
 }
 

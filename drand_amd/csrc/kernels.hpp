@@ -144,19 +144,23 @@ hipError_t launch_partial_meta(const uint32_t* off, size_t n_rounds, const uint3
                                uint8_t* status, hipStream_t st);
 hipError_t launch_clamp_group(const uint32_t* share_idx, size_t np, uint32_t hi, uint32_t* grp, hipStream_t st);
 hipError_t launch_ok_from_status(const uint8_t* status, size_t np, uint8_t* ok, hipStream_t st);
-// per round: Recover's selection + Lagrange coefficients (sel/key: t words, den: 8t words, lam: 48t words per round);
-// lam_set[j] = the round whose lambda rows round j uses (0 when its selected indices equal round 0's, else j)
+// per round: Recover's selection + Lagrange coefficients (sel/key: t words, den: 8t words, lam: lam_words() t words
+// per round); lam_set[j] = the round whose lambda rows round j uses (0 when its selected indices equal round 0's, else
+// j); *own = the number of rounds j > 0 with their own rows (device word)
+size_t lam_words();
 hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const uint32_t* share_idx, int t, size_t n_rounds,
                                   uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint32_t* lam_set, uint8_t* rok,
-                                  hipStream_t st);
-// tbl (G2): per valid partial (ok) P, 3P, 5P, 7P affine 28-bit (256 words each) from the partials' affine points
-// (12 x 32-bit AOS); zs: wnaf_table_scratch_bytes(n) of scratch (the batched inversion's Z's); unused for G1
-hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, uint32_t* tbl, uint32_t* zs,
+                                  uint32_t* own, hipStream_t st);
+// tbl (G2): per valid partial (ok) the odd multiples P, 3P, ..., (2 entries - 1) P affine 28-bit (entries = 4 or 8,
+// 64 words each) from the partials' affine points (12 x 32-bit AOS); zs: wnaf_table_scratch_bytes(n, entries) of
+// scratch (the batched inversion's Z's); unused for G1
+hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, int entries, uint32_t* tbl, uint32_t* zs,
                                 hipStream_t st);
-size_t wnaf_table_scratch_bytes(size_t n);
+size_t wnaf_table_scratch_bytes(size_t n, int entries);
 // tmp: lagrange_tmp_bytes(sig_g2) of scratch for the sliced last wave of workgroups (null: no slicing)
+// entries: the G2 tables' width (8: waves whose rounds use different bases run the regular windows)
 hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam, const uint32_t* lam_set, const uint8_t* ok,
-                           int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, uint32_t* out,
+                           int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, int entries, uint32_t* out,
                            uint32_t* tmp, hipStream_t st);
 size_t lagrange_tmp_bytes(int sig_g2);
 hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, hipStream_t st);

@@ -38,3 +38,37 @@ def test_wnaf4_digits():
             assert b - last >= 4
             last = b
         assert total == lam
+
+
+def reg4_nibbles(w):
+    """fr.hpp fr_reg4: 64 odd nonzero signed 4-bit window digits of 0 < w < r (an even w recoded as r - w, negated)"""
+    R = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    flip = w % 2 == 0
+    k = R - w if flip else w
+    out = []
+    for i in range(64):
+        if i < 63:
+            d = (k & 31) - 16
+            k = (k - d) >> 4
+        else:
+            d = k
+        if flip:
+            d = -d
+        out.append(((abs(d) - 1) // 2) | (8 if d < 0 else 0))
+    return out
+
+
+def test_reg4_digits():
+    """The regular recoding k_lagrange's divergent waves use: every digit odd and nonzero with |d| <= 15 (table P .. 15P),
+    sum d_i 16^i == lambda mod r (== lambda, or -(r - lambda) for an even lambda), for lambda < r."""
+    R = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    rng = random.Random(12)
+    for lam in [1, 2, 3, 15, 16, 17, 255, 256, R - 1, R - 2, (1 << 254) + 3, (1 << 254)] + \
+            [rng.randrange(1, R) for _ in range(3000)]:
+        nib = reg4_nibbles(lam)
+        total = 0
+        for i, v in enumerate(nib):
+            mag = 2 * (v & 7) + 1
+            assert 1 <= mag <= 15
+            total += (-mag if v & 8 else mag) * 16 ** i
+        assert total % R == lam, lam
