@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--rounds-per-gpu", type=int, default=0,
                     help="weak scaling: rounds per GPU (default 1048576 when --total-rounds is not given)")
     ap.add_argument("--scheme", default="bls-unchained-g1-rfc9380")
-    ap.add_argument("--cpu-sample-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-sample-seconds", type=float, default=8.0,
+                    help="wall time of the bounded CPU-baseline sample (after the GPU legs; kept short so the GPU work is "
+                         "not a small share of the run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stage-times", action="store_true",
                     help="leave the library's HIP-event stage timing off inside the timed region")
