@@ -758,7 +758,7 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
   return hipGetLastError();
 }
 
-// launch_msm on the 28-bit points of launch_msm_prep28: both point sets, one reduction pass over 2 x ngroups
+// the RLC MSM on the 28-bit points of launch_msm_prep28: both point sets, one reduction pass over 2 x ngroups
 hipError_t launch_msm28(int sig_g2, const msm_geom& g, const uint32_t* entries, size_t m, size_t ngroups, const uint4* scal,
                         const uint32_t* S, const uint32_t* Q, msm_ws& ws, uint32_t* outA, uint32_t* outB, hipStream_t st,
                         const uint8_t* skip, bool presorted) {
