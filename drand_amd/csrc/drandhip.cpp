@@ -1002,7 +1002,10 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
                                   w->q28.as<uint32_t>(), st, 2));
     dh::msm_geom gA = geom_for(std::max<size_t>(np, 1), parts);
     gA.half_stride = (uint32_t)np;
-    size_t avg = std::max<size_t>(1, np / std::max(1, n_nodes));
+    // window geometry of the per-signer groups from the partials per signer that answered: at least t signers answer
+    // a recoverable round and the same ones usually answer every round, so np / t (np / n_nodes undercounted a group
+    // by n_nodes / t and picked 3 windows of c = 15 where 2 of c = 16 do a third fewer bucket additions)
+    size_t avg = std::max<size_t>(1, np / (size_t)std::max(1, std::min(t, n_nodes)));
     dh::msm_geom gB = geom_for(avg, parts);
     while (gB.c > 3 && (size_t)n_nodes * gB.nwin * gB.nbuck > ((size_t)1 << 24))
       gB = geom_for(std::max<size_t>(1, ((size_t)1 << (gB.c + 1)) / parts), parts);

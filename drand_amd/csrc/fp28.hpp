@@ -385,24 +385,18 @@ DH_DEV bool g1_in_subgroup28(LD ld) {
     const aff<fp> p = ld();
     const f28 x = f28_from_fp(p.x), y = f28_from_fp(p.y);
     j28 acc{x, y, f28_one(), false};
-    // the doublings as runs between |u|'s set bits (62, 60, 57, 48, 16: 1, 2, 3, 9, 32, 16), each an inner loop with
-    // the addition after it, so the doublings' loop carries none of the addition's live values
 #pragma unroll 1
-    for (int r = 0; r < 6; r++) {
-      const int k = r == 0 ? 1 : r == 1 ? 2 : r == 2 ? 3 : r == 3 ? 9 : r == 4 ? 32 : 16;
-#pragma unroll 1
-      for (int i = 0; i < k; i++) acc = j28_dbl<true>(acc);
-      if (r < 5) acc = j28_madd(acc, x, y);
+    for (int b = 62; b >= 0; b--) {
+      acc = j28_dbl<true>(acc);
+      if ((cst::U_ABS >> b) & 1) acc = j28_madd(acc, x, y);
     }
     t = acc;  // (26, 18, 4): the last step is a doubling
   }
   j28 acc = t;
 #pragma unroll 1
-  for (int r = 0; r < 6; r++) {
-    const int k = r == 0 ? 1 : r == 1 ? 2 : r == 2 ? 3 : r == 3 ? 9 : r == 4 ? 32 : 16;
-#pragma unroll 1
-    for (int i = 0; i < k; i++) acc = j28_dbl<true>(acc);
-    if (r < 5) acc = j28_add(acc, t);
+  for (int b = 62; b >= 0; b--) {
+    acc = j28_dbl<true>(acc);
+    if ((cst::U_ABS >> b) & 1) acc = j28_add(acc, t);
   }
   if (acc.inf) return false;  // phi(P) is finite
   asm volatile("" ::: "memory");      // reload P rather than keep it live through the loop
