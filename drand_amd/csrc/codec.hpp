@@ -112,15 +112,23 @@ DH_DEV void st_be48(uint8_t* out, const fp& canon) {
   for (int i = 0; i < 12; i++) *(uint32_t*)(out + 44 - 4 * i) = __builtin_bswap32(canon.v[i]);
 }
 
+// compressed encodings of a finite affine point / of a Jacobian point (infinity: the 0xc0 encoding)
+DH_DEV void g1_compress_aff(uint8_t* out, const aff<fp>& a) {
+  st_be48(out, fp_from_mont(a.x));
+  out[0] |= 0x80 | (fp_lex_gt_half(a.y) ? 0x20 : 0);
+}
+DH_DEV void g2_compress_aff(uint8_t* out, const aff<fp2>& a) {
+  st_be48(out, fp_from_mont(a.x.c1));
+  st_be48(out + 48, fp_from_mont(a.x.c0));
+  out[0] |= 0x80 | (fp2_lex_largest(a.y) ? 0x20 : 0);
+}
 DH_DEV void g1_compress(uint8_t* out, const jac<fp>& p) {
   if (jac_is_inf(p)) {
     for (int i = 0; i < 48; i++) out[i] = 0;
     out[0] = 0xc0;
     return;
   }
-  aff<fp> a = jac_to_aff(p);
-  st_be48(out, fp_from_mont(a.x));
-  out[0] |= 0x80 | (fp_lex_gt_half(a.y) ? 0x20 : 0);
+  g1_compress_aff(out, jac_to_aff(p));
 }
 
 DH_DEV void g2_compress(uint8_t* out, const jac<fp2>& p) {
@@ -129,10 +137,7 @@ DH_DEV void g2_compress(uint8_t* out, const jac<fp2>& p) {
     out[0] = 0xc0;
     return;
   }
-  aff<fp2> a = jac_to_aff(p);
-  st_be48(out, fp_from_mont(a.x.c1));
-  st_be48(out + 48, fp_from_mont(a.x.c0));
-  out[0] |= 0x80 | (fp2_lex_largest(a.y) ? 0x20 : 0);
+  g2_compress_aff(out, jac_to_aff(p));
 }
 
 }  // namespace dh

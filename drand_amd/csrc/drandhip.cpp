@@ -1124,17 +1124,18 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
   HIP_TRY(hipMemcpyAsync(rok.data(), w->r_rok.p, n_rounds, hipMemcpyDeviceToHost, st));
   // 14./15. compress, then VerifyRecovered (chainstore.go:207) as one batch against the group key (commit 0)
   HIP_TRY(w->r_sigbytes.ensure(n_rounds * sl));
-  HIP_TRY(dh::launch_compress(g2, w->r_sig.as<uint32_t>(), n_rounds, w->r_sigbytes.as<uint8_t>(), st));
+  HIP_TRY(w->r_status2.ensure(n_rounds));
+  HIP_TRY(w->r_aff2.ensure(n_rounds * aw * 4));
+  // the compression also leaves the affine points and decode statuses the VerifyRecovered batch takes (decoding the
+  // bytes again — an Fp(2) square root and a subgroup test per round — would return the same points)
+  HIP_TRY(dh::launch_compress(g2, w->r_sig.as<uint32_t>(), n_rounds, w->r_sigbytes.as<uint8_t>(), w->r_aff2.as<uint32_t>(),
+                              w->r_status2.as<uint8_t>(), st));
   HIP_TRY(hipMemcpyAsync(sig_out, w->r_sigbytes.p, n_rounds * sl, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   // verify through the regular batch path (messages are given digests: use the per-round hash points)
   std::vector<uint8_t> vv(n_rounds, 0);
   {
-    HIP_TRY(w->r_status2.ensure(n_rounds));
-    HIP_TRY(w->r_aff2.ensure(n_rounds * aw * 4));
     HIP_TRY(w->r_entries2.ensure(n_rounds * 4));
-    HIP_TRY(dh::launch_prep(g2, w->r_sigbytes.as<uint8_t>(), sl, n_rounds, w->r_status2.as<uint8_t>(),
-                            w->r_aff2.as<uint32_t>(), nullptr, st));
     HIP_TRY(w->r_scal.ensure(std::max(np, n_rounds) * 16 + 16));  // rounds may outnumber the partials
     HIP_TRY(dh::launch_scalars(d_seed, n_rounds, w->r_status2.as<uint8_t>(), w->r_scal.as<uint4>(), parts, st));
     HIP_TRY(dh::launch_iota(w->r_entries2.as<uint32_t>(), n_rounds, st));

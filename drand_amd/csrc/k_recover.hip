@@ -528,12 +528,27 @@ __global__ __launch_bounds__(64) void k_lagrange_sum(const uint32_t* __restrict_
 }
 
 template <class F>
-__global__ __launch_bounds__(64) void k_compress(const uint32_t* __restrict__ pts, size_t n, uint8_t* __restrict__ out) {
+__global__ __launch_bounds__(64) void k_compress(const uint32_t* __restrict__ pts, size_t n, uint8_t* __restrict__ out,
+                                                 uint32_t* __restrict__ aff_out, uint8_t* __restrict__ status_out) {
   size_t j = gtid();
   if (j >= n) return;
   jac<F> p = ld_jac_aos<F>(pts, j);
-  if constexpr (sizeof(F) == sizeof(fp)) g1_compress(out + 48 * j, p);
-  else g2_compress(out + 96 * j, p);
+  const bool inf = jac_is_inf(p);
+  if (inf) {
+    if constexpr (sizeof(F) == sizeof(fp)) g1_compress(out + 48 * j, p);
+    else g2_compress(out + 96 * j, p);
+  }
+  const aff<F> a = inf ? aff<F>{F{}, F{}} : jac_to_aff(p);
+  if (!inf) {
+    if constexpr (sizeof(F) == sizeof(fp)) g1_compress_aff(out + 48 * j, a);
+    else g2_compress_aff(out + 96 * j, a);
+  }
+  // the affine point and decode status VerifyRecovered's batch needs (what decoding these bytes gives: the point is a
+  // combination of subgroup-checked partials, so it is in the subgroup; infinity is rejected like a decoded one)
+  if (aff_out) {
+    st_aff_aos<F>(aff_out, j, a);
+    status_out[j] = inf ? DEC_BAD : DEC_OK;
+  }
 }
 
 // assemble the pairs of the batched VerifyPartial check:
@@ -673,10 +688,11 @@ hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam,
   return hipGetLastError();
 }
 
-hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, hipStream_t st) {
+hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, uint32_t* aff_out, uint8_t* status_out,
+                           hipStream_t st) {
   if (!n) return hipSuccess;
-  if (sig_g2) hipLaunchKernelGGL(k_compress<fp2>, dim3(nblk(n, 64)), dim3(64), 0, st, pts, n, out);
-  else hipLaunchKernelGGL(k_compress<fp>, dim3(nblk(n, 64)), dim3(64), 0, st, pts, n, out);
+  if (sig_g2) hipLaunchKernelGGL(k_compress<fp2>, dim3(nblk(n, 64)), dim3(64), 0, st, pts, n, out, aff_out, status_out);
+  else hipLaunchKernelGGL(k_compress<fp>, dim3(nblk(n, 64)), dim3(64), 0, st, pts, n, out, aff_out, status_out);
   return hipGetLastError();
 }
 

@@ -163,7 +163,10 @@ hipError_t launch_lagrange(int sig_g2, const uint32_t* sel, const uint32_t* lam,
                            int t, size_t n_rounds, const uint32_t* sig_aff, const uint32_t* tbl, int entries, uint32_t* out,
                            uint32_t* tmp, hipStream_t st);
 size_t lagrange_tmp_bytes(int sig_g2);
-hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, hipStream_t st);
+// compressed bytes of n Jacobian points; aff_out / status_out (nullable): their affine form and a decode status
+// (DEC_OK, DEC_BAD for infinity) — what decoding the bytes of a subgroup point gives
+hipError_t launch_compress(int sig_g2, const uint32_t* pts, size_t n, uint8_t* out, uint32_t* aff_out, uint8_t* status_out,
+                           hipStream_t st);
 hipError_t launch_recover_pairs(int sig_g2, const uint32_t* shares, const uint32_t* B, const uint32_t* A, int n_nodes,
                                 uint32_t* P, uint32_t* Q, hipStream_t st);
 
