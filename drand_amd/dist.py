@@ -8,13 +8,15 @@
   own shard (e.g. each streams its range from a different peer). A missing round start-1 travels as MISSING_HALO,
   and the next rank reports its first round missing, as the trimmed store's Get would (trimmed.go:183-187).
 * Node-wide check: every rank computes its level-0 RLC sums (A_g, B_g) with dh_batch_begin; one all-gather of
-  those 2 points (plus a status byte) per rank over RCCL (xGMI), then ONE pairing check of the sums for the whole
-  node (dh_check_partials) and dh_batch_finish: all ranks accept, or each bisects its own shard. A rank whose
+  those 2 points (plus a status word) per rank over RCCL (xGMI) on the batch's own library stream, then ONE pairing
+  check of the sums for the whole node (dh_batch_check, queued on that stream) and dh_batch_finish, the batch's one
+  host wait: all ranks accept, or each bisects its own shard. A rank whose
   dh_batch_begin failed still takes part in the exchange (identity sums, status 1), so every rank abandons the
   batch together instead of blocking in the collective. No data-path collective besides that (the per-round data
   never leaves its GPU).
 * Verdicts: packed bitmaps all-gathered once at the end (gather_verdicts).
-* replay_shard: the sharded CheckPastBeacons (chain/beacon/sync_manager.go:170-235) built from the pieces above.
+* replay_shard: the sharded CheckPastBeacons (chain/beacon/sync_manager.go:170-235) built from the pieces above;
+  recover_shard: tbls Recover with its rounds sharded (no exchange before the gather).
 The collectives use torch.distributed: backend "nccl" (= RCCL) with device tensors, "gloo" with host tensors
 (the CPU tests, and N ranks rehearsed on one GPU).
 """
@@ -156,7 +158,7 @@ def gather_verdicts(bits, world, group=None, failed=None):
 
 def gather_partials(local, world, group=None):
     """All-gather each rank's level-0 partial sums (dh_partial_bytes bytes, uint8 tensor) into one
-    (world * bytes) tensor in rank order: the input of dh_check_partials."""
+    (world * bytes) tensor in rank order: the input of dh_batch_check (or of the standalone dh_check_partials)."""
     import torch
     import torch.distributed as dist
     if world == 1:
