@@ -124,6 +124,8 @@ struct worker {
   // fault density (faults per round) the last bisection of this worker observed at its first level: a replay's
   // consecutive windows fail alike, so a dense one starts its next bisection with smaller groups (next_group_size)
   double fault_density = 0;
+  // set by dh_batch_begin while it queues a node batch on one stream (node_one_stream): no tail-stream handoff
+  bool begin_one_stream = false;
   void release_all() {
     dbuf* all[] = {&s28, &q28, &entries_alt, &cflags, &crank, &cscan, &status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &h2c_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
@@ -722,7 +724,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     // while the per-round kernels decode and hash (its ~1 ms of small kernels left the one-call latency path).
     // Every round then carries a scalar; the bucket passes skip rounds whose status is not DEC_OK. A batch that skips
     // level 0 (skip0) has no level-0 sort.
-    presorted = w->tail && st == w->stream && !skip0;
+    presorted = w->tail && st == w->stream && !skip0 && !(mode == VM_BEGIN && w->begin_one_stream);
     if (presorted) {
       hipStream_t ts = w->tail;
       HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, ts));
@@ -770,7 +772,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     if (!presorted) HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
   }
   // the tail (MSM, checks, bisection) runs on the worker's high-priority stream, after the per-round kernels
-  if (w->tail && st == w->stream) {
+  if (w->tail && st == w->stream && !(mode == VM_BEGIN && w->begin_one_stream)) {
     if (mode <= VM_BEGIN) {
       HIP_TRY(hipEventRecord(w->handoff, st));
       HIP_TRY(hipStreamWaitEvent(w->tail, w->handoff, 0));
@@ -1438,6 +1440,21 @@ int dh_partial_bytes(int scheme) {
   return (int)(partial_words(sig_on_g2(scheme)) * 4);
 }
 
+// A node batch queues its level-0 tail, record, exchange and check on the worker's normal stream behind its per-round
+// kernels, with the level-0 sort there too, instead of handing the tail to the high-priority stream behind an event
+// wait: 8 batches in flight, one GPU (gpurun_out r04y, one box): 1M rounds 25.75 -> 26.36 M/s (local check 26.48),
+// 131k rounds 18.09 -> 21.42 M/s. A high-priority queue holding a batch's pending wait for the whole of its per-round
+// kernels cost the other batches' dispatch (the local path's host wait before queueing its tail is the same fix).
+// DRANDHIP_NODE_ONE_STREAM=0 restores the tail-stream handoff (comparison runs).
+static bool node_one_stream() {
+  static const bool v = [] {
+    const char* e = getenv("DRANDHIP_NODE_ONE_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+static hipStream_t batch_stream(worker* w) { return node_one_stream() ? w->stream : w->tail; }
+
 int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t* d_rounds, const uint8_t* d_sigs,
                    size_t sig_stride, const uint8_t* d_prevs, size_t prev_stride, const uint32_t* d_prev_lens, size_t n,
                    uint8_t* d_verdict_out, uint8_t* d_rand_out, uint64_t seed, void* hip_stream, dh_batch** batch_out,
@@ -1473,13 +1490,16 @@ int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t*
   b->d_rand = d_rand_out;
   b->st = w->stream;
   const size_t jw = sig_on_g2(scheme) ? JAC_WORDS_G2 : JAC_WORDS_G1;
-  if (!rc)
+  if (!rc) {
+    w->begin_one_stream = node_one_stream();
     rc = verify_core(w, scheme, pk, pk_len, d_rounds, d_sigs, sig_stride, d_prevs, prev_stride, d_prev_lens, n, d_verdict_out,
                      d_rand_out, seed, b->st, nullptr, nullptr, VM_BEGIN);
+    w->begin_one_stream = false;
+  }
   if (!rc) {
-    // the record (A, B, status 0) on the tail stream, where the level-0 MSM wrote the sums (an empty batch
+    // the record (A, B, status 0) on the batch stream, where the level-0 MSM wrote the sums (an empty batch
     // contributes the identity, Z = 0)
-    hipStream_t ts = w->tail;
+    hipStream_t ts = batch_stream(w);
     const bool ok = (n ? hipMemcpyAsync(d_partials_out, w->outA.p, jw * 4, hipMemcpyDeviceToDevice, ts) == hipSuccess &&
                              hipMemcpyAsync(d_partials_out + jw * 4, w->outB.p, jw * 4, hipMemcpyDeviceToDevice, ts) == hipSuccess
                        : hipMemsetAsync(d_partials_out, 0, 2 * jw * 4, ts) == hipSuccess) &&
@@ -1498,9 +1518,9 @@ int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t*
   return DH_OK;
 }
 
-// the node-wide check of k gathered records on worker w's tail stream: sum, one pairing check, res = w->node_res
-static int queue_node_check(worker* w, bool g2, const uint8_t* pk, size_t pk_len, const uint8_t* d_partials, size_t k) {
-  hipStream_t ts = w->tail;
+// the node-wide check of k gathered records on the batch stream: sum, one pairing check, res = w->node_res
+static int queue_node_check(worker* w, bool g2, const uint8_t* pk, size_t pk_len, const uint8_t* d_partials, size_t k,
+                            hipStream_t ts) {
   int rc = ensure_key(w, g2, pk, pk_len, ts);
   if (rc) return rc;
   const size_t jw = g2 ? JAC_WORDS_G2 : JAC_WORDS_G1;
@@ -1514,20 +1534,21 @@ static int queue_node_check(worker* w, bool g2, const uint8_t* pk, size_t pk_len
   return DH_OK;
 }
 
-void* dh_batch_stream(dh_batch* b) { return b ? (void*)b->L->w->tail : nullptr; }
+void* dh_batch_stream(dh_batch* b) { return b ? (void*)batch_stream(b->L->w) : nullptr; }
 
 int dh_batch_check(dh_batch* b, const uint8_t* d_partials, size_t k, void* hip_stream) {
   if (!b || !d_partials || !k) return fail(DH_EINVAL, "bad node-check arguments");
   worker* w = b->L->w;
   const bool g2 = sig_on_g2(b->scheme);
-  if (hip_stream && (hipStream_t)hip_stream != w->tail) {  // the gathered records are produced on the caller's stream
+  hipStream_t bs = batch_stream(w);
+  if (hip_stream && (hipStream_t)hip_stream != bs) {  // the gathered records are produced on the caller's stream
     HIP_TRY(hipEventRecord(w->gath_ready, (hipStream_t)hip_stream));
-    HIP_TRY(hipStreamWaitEvent(w->tail, w->gath_ready, 0));
+    HIP_TRY(hipStreamWaitEvent(bs, w->gath_ready, 0));
   }
-  int rc = queue_node_check(w, g2, b->pk.data(), b->pk.size(), d_partials, k);
+  int rc = queue_node_check(w, g2, b->pk.data(), b->pk.size(), d_partials, k, bs);
   if (rc) return rc;
   // passed: every decoded round of this batch is valid, marked on the device
-  HIP_TRY(dh::launch_node_mark(b->n, w->node_res.as<uint8_t>(), w->status.as<uint8_t>(), b->d_verdict, w->tail));
+  HIP_TRY(dh::launch_node_mark(b->n, w->node_res.as<uint8_t>(), w->status.as<uint8_t>(), b->d_verdict, bs));
   b->checked = true;
   return DH_OK;
 }
@@ -1543,7 +1564,7 @@ int dh_check_partials(int scheme, const uint8_t* pk, size_t pk_len, const uint8_
   worker* w = L.w;
   int rc = set_device_and_stream(w);
   if (rc) return rc;
-  rc = queue_node_check(w, g2, pk, pk_len, d_partials, k);
+  rc = queue_node_check(w, g2, pk, pk_len, d_partials, k, w->tail);
   if (rc) return rc;
   uint8_t res[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(res, w->node_res.p, 2, hipMemcpyDeviceToHost, w->tail));
@@ -1563,8 +1584,8 @@ int dh_batch_finish(dh_batch* b, int node_pass, uint64_t stats_out[4]) {
     uint8_t res = 0;
     if (!b->checked) {
       rc = fail(DH_EINVAL, "dh_batch_finish(DH_NODE_CHECKED) without dh_batch_check");
-    } else if (hipMemcpyAsync(&res, w->node_res.as<uint8_t>() + 2, 1, hipMemcpyDeviceToHost, w->tail) != hipSuccess ||
-               hipStreamSynchronize(w->tail) != hipSuccess) {
+    } else if (hipMemcpyAsync(&res, w->node_res.as<uint8_t>() + 2, 1, hipMemcpyDeviceToHost, batch_stream(w)) != hipSuccess ||
+               hipStreamSynchronize(batch_stream(w)) != hipSuccess) {
       rc = fail(DH_EDEVICE, "reading the node-wide check failed");
     } else if (res == 2) {
       rc = fail(DH_EABANDONED, "node batch abandoned: dh_batch_begin failed on another rank");
