@@ -697,6 +697,11 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   const size_t wsw = g2 ? 96 : 48;
 
   timed_launches T(st);
+  // the whole batch on st (no tail-stream handoff, no level-0 presort there): a node batch's begin (begin_one_stream).
+  // A local batch keeps the handoff after its host wait: measured on one stream too (gpurun_out r04aa), 1M rounds
+  // 26.58 -> 26.41 M/s and one 1M call 46.2 -> 47.5 ms (the presort no longer overlaps the per-round kernels), 131k
+  // rounds 20.76 -> 21.46 M/s.
+  const bool one_stream = mode == VM_BEGIN && w->begin_one_stream;
   bool presorted = false;  // level-0 sorted lists already built on the tail stream
   // A local batch on a worker whose last bisection saw dense faults skips level 0: its one group is expected to fail,
   // so the batch starts at the dense ladder's 256-round groups (their check also answers "is the batch clean": a
@@ -724,7 +729,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     // while the per-round kernels decode and hash (its ~1 ms of small kernels left the one-call latency path).
     // Every round then carries a scalar; the bucket passes skip rounds whose status is not DEC_OK. A batch that skips
     // level 0 (skip0) has no level-0 sort.
-    presorted = w->tail && st == w->stream && !skip0 && !(mode == VM_BEGIN && w->begin_one_stream);
+    presorted = w->tail && st == w->stream && !skip0 && !one_stream;
     if (presorted) {
       hipStream_t ts = w->tail;
       HIP_TRY(hipMemcpyAsync(d_seed, seedw, 32, hipMemcpyHostToDevice, ts));
@@ -768,11 +773,11 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     // run, and with 8 batches in flight (16+ streams on 16 hardware queues) a queue blocked on such a wait holds up
     // the streams that share it (quicknet 1M: 25.5-25.9 M/s without this wait, 26.4-26.5 with it; DRANDHIP_PREP_SYNC=0
     // drops it for comparison).
-    if (mode == VM_FULL && w->tail && st == w->stream && prep_sync()) HIP_TRY(hipStreamSynchronize(st));
+    if (mode == VM_FULL && w->tail && st == w->stream && !one_stream && prep_sync()) HIP_TRY(hipStreamSynchronize(st));
     if (!presorted) HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, st));
   }
   // the tail (MSM, checks, bisection) runs on the worker's high-priority stream, after the per-round kernels
-  if (w->tail && st == w->stream && !(mode == VM_BEGIN && w->begin_one_stream)) {
+  if (w->tail && st == w->stream && !one_stream) {
     if (mode <= VM_BEGIN) {
       HIP_TRY(hipEventRecord(w->handoff, st));
       HIP_TRY(hipStreamWaitEvent(w->tail, w->handoff, 0));
