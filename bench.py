@@ -75,6 +75,9 @@ def parse():
                     help="GPU_MAX_HW_QUEUES for this process (0: keep the environment's)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse N ranks on one GPU with host-staged collectives")
+    ap.add_argument("--exchange", choices=["auto", "always"], default="auto",
+                    help="always: run the node step's collectives at N = 1 too, over a one-rank process group (the "
+                         "RCCL branch rehearsed on one GPU; RCCL takes one rank per GPU)")
     return ap.parse_args()
 
 
@@ -171,7 +174,14 @@ def main():
         raise SystemExit("dh_init failed: %s" % _lib.last_error())
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    pg = world > 1 or args.exchange == "always"  # a process group runs the collectives
+    xchg = True if args.exchange == "always" else None  # dist._exchanges: collectives at world 1 too
+    if pg:
+        if "MASTER_ADDR" not in os.environ:  # a one-rank group without a launcher
+            so = socket.socket()
+            so.bind(("127.0.0.1", 0))
+            os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(so.getsockname()[1])
+            so.close()
         if gloo:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
@@ -241,14 +251,14 @@ def main():
             t0 = time.perf_counter()
             pending.append((slot, begin_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot], d_rand[slot],
                                                    d_part[slot], world, None, stage_host=gloo, rank=rank,
-                                                   inputs_ready=True)))
+                                                   inputs_ready=True, exchange=xchg)))
             ht["begin_exchange_check"] += time.perf_counter() - t0
         while pending:
             retire()
         torch.cuda.synchronize()
-        if world > 1 and gather and k_steps:
+        if pg and gather and k_steps:
             b = torch.cat(bits)
-            gather_verdicts(b.cpu() if gloo else b, world)
+            gather_verdicts(b.cpu() if gloo else b, world, exchange=xchg)
         torch.cuda.synchronize()
 
     def run_steps(k_steps, streams, gather=True):
@@ -274,9 +284,9 @@ def main():
             th.join()
         if errs:
             raise errs[0]
-        if world > 1 and gather and k_steps:  # whole-node verdict bitmaps: one all-gather after the batches
+        if pg and gather and k_steps:  # whole-node verdict bitmaps: one all-gather after the batches
             b = torch.cat(bits)
-            gather_verdicts(b.cpu() if gloo else b, world)
+            gather_verdicts(b.cpu() if gloo else b, world, exchange=xchg)
         torch.cuda.synchronize()
 
     def profile_read():
@@ -290,13 +300,13 @@ def main():
     run_steps(warm_batches, S)
     lib.dh_profile(0 if args.no_stage_times else 1)
     state["node_host_s"] = collections.Counter()  # the timed region's host time per pipeline phase
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run_steps(args.steps, S)
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     prof = profile_read()
@@ -354,7 +364,7 @@ def main():
         del d_r4, d_s4, d_v4
         lib.dh_set_split(0, 1)
 
-    if world > 1:
+    if pg:
         t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device="cpu" if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, bad = float(t[0]), float(t[1])
@@ -400,8 +410,9 @@ def main():
         "config": {"workload": "%s batch verify of a %d-round chain, %s" % (
                        sch.name, total, "%d rounds per GPU" % n if weak else "split over %d GPU(s)" % world),
                    "scheme": sch.name, "rounds_total": total, "rounds_per_gpu": n, "global_batch": total,
-                   "parallelism": "round-shard x%d%s" % (world, (", node-wide RLC check (%s all-gather)" % (
-                       "gloo, host-staged" if gloo else "RCCL")) if node_check else "")},
+                   "parallelism": "round-shard x%d%s" % (world, (", node-wide RLC check (%s)" % (
+                       ("%s all-gather%s" % ("gloo, host-staged" if gloo else "RCCL", ", one-rank group" if world == 1
+                                             else "")) if pg else "one rank, no exchange")) if node_check else "")},
         "roofline": roof,
         "node_roofline_frac": round(value * executed / (peak * world), 4),
         "node_roofline_basis": "executed kernel work %d M/beacon (prep_sig + prep_msg + MSM, bench/workmodel.json "
@@ -418,7 +429,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sch.name, pk, rounds, sigs, args.cpu_sample_seconds)
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

@@ -78,6 +78,13 @@ def shard_beacons(store, rank, world, first, last):
     return rounds, sigs, prevs, missing
 
 
+def _exchanges(world, exchange):
+    """Whether a node step runs its collective: with more than one rank, or at world 1 when the caller asks for it
+    (exchange=True: the all-gathers run over a one-rank process group, which rehearses the device-side RCCL branch on
+    one GPU — two ranks cannot share a GPU under RCCL)."""
+    return world > 1 if exchange is None else bool(exchange)
+
+
 def _collective_device(group):
     """Where the collective's tensors live: the current GPU under nccl (RCCL), the host under gloo."""
     import torch
@@ -87,14 +94,14 @@ def _collective_device(group):
     return torch.device("cpu")
 
 
-def exchange_halo(last_signature, rank, world, group=None):
+def exchange_halo(last_signature, rank, world, group=None, exchange=None):
     """Rank r receives rank r-1's last stored signature (a stored record may have any length): an all-gather of
     the record lengths, then one of slots that fit the longest, on the device under nccl. `last_signature` is None
     when this shard's last round is missing from the store: the next rank then gets MISSING_HALO. Rank 0 (and
     world 1) gets None."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if not _exchanges(world, exchange):
         return None
     dev = _collective_device(group)
     missing = last_signature is None
@@ -131,14 +138,14 @@ class NodeFailure(RuntimeError):
     """Some rank failed its part of a node-wide step; raised on every rank after the collective."""
 
 
-def gather_verdicts(bits, world, group=None, failed=None):
+def gather_verdicts(bits, world, group=None, failed=None, exchange=None):
     """All-gather the ranks' bitmaps (sizes may differ by one byte under strong scaling); returns them in rank
     order, each trimmed to its own length. `failed` (a message, or None) marks this rank's part as failed: the flag
     travels with the sizes, so a rank that failed after the node check still joins the collective and every rank
     raises NodeFailure instead of waiting for it."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if not _exchanges(world, exchange):
         if failed:
             raise NodeFailure(failed)
         return [bits]
@@ -156,12 +163,12 @@ def gather_verdicts(bits, world, group=None, failed=None):
     return [o[:int(k[0])] for o, k in zip(out, sizes)]
 
 
-def gather_partials(local, world, group=None):
+def gather_partials(local, world, group=None, exchange=None):
     """All-gather each rank's level-0 partial sums (dh_partial_bytes bytes, uint8 tensor) into one
     (world * bytes) tensor in rank order: the input of dh_batch_check (or of the standalone dh_check_partials)."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if not _exchanges(world, exchange):
         return local
     out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
     if local.is_cuda:
@@ -220,7 +227,7 @@ class NodeBatch:
 
 def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, partials, world, group=None,
                      d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=None, rank=None,
-                     inputs_ready=False):
+                     inputs_ready=False, exchange=None):
     """Begin one batch under the node-wide check and queue its exchange and check: dh_batch_begin
     (per-round kernels + level-0 MSM, record written into `partials`, a uint8 device tensor of dh_partial_bytes) ->
     all-gather of the records -> dh_batch_check (ONE pairing check of the summed records, on this batch's worker).
@@ -229,7 +236,8 @@ def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, pa
     crosses streams; the inputs are ordered after torch's current stream (unless inputs_ready). Under gloo
     (stage_host) the records go through host memory. A rank whose dh_batch_begin failed still takes part in the exchange with a record whose
     status word is 1, so every rank's check sees it and abandons the batch (finish raises everywhere) instead of
-    blocking in the collective. Returns a NodeBatch; its finish() waits for the verdicts."""
+    blocking in the collective. exchange=True runs the all-gather at world 1 too (_exchanges). Returns a NodeBatch;
+    its finish() waits for the verdicts."""
     import torch
     import torch.distributed as dist
     from . import _lib
@@ -266,13 +274,13 @@ def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, pa
         if err is not None:
             partials.zero_()
             partials[_status_offset(pb)] = 1
-        if world == 1:
+        if not _exchanges(world, exchange):
             gathered = partials
         else:
             if stage_host is None:
                 stage_host = not dist.get_backend(group) == "nccl"
             slot = partials.cpu() if stage_host else partials
-            gathered = gather_partials(slot, world, group)
+            gathered = gather_partials(slot, world, group, exchange)
             if stage_host:
                 gathered = gathered.to(partials.device)
     if err is not None:
@@ -286,16 +294,16 @@ def begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, pa
 
 
 def verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, partials, world, group=None,
-                      d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=None, rank=None):
+                      d_prevs=None, prev_stride=0, d_prev_lens=None, seed=0, stage_host=None, rank=None, exchange=None):
     """One batch of this rank's shard under the node-wide check, to completion (begin_node_batch + finish). Returns
     the node-wide pass flag; raises on every rank if any rank's dh_batch_begin failed."""
     return begin_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, d_rand, partials, world, group,
                             d_prevs=d_prevs, prev_stride=prev_stride, d_prev_lens=d_prev_lens, seed=seed,
-                            stage_host=stage_host, rank=rank).finish()
+                            stage_host=stage_host, rank=rank, exchange=exchange).finish()
 
 
 def replay_shard(lib, scheme, pk, first, last, sig_of, rank, world, group=None, prev_of_first=None, seed=0,
-                 device=None, stage_host=None):
+                 device=None, stage_host=None, exchange=None):
     """This rank's part of a sharded chain replay (CheckPastBeacons' verification over the node,
     /root/reference/chain/beacon/sync_manager.go:191-225, sharded as SURVEY.md §8e): rounds first..last are split
     with shard_range, and `sig_of` maps each round of this rank's range to its stored signature (a round absent
@@ -304,7 +312,8 @@ def replay_shard(lib, scheme, pk, first, last, sig_of, rank, world, group=None, 
     (exchange_halo), or from `prev_of_first` on rank 0 (the stored record of round first-1: the genesis seed when
     first = 1). A round is faulty when it is missing, its previous record is missing (chained), or it fails
     VerifyBeacon. The present rounds are verified in one batch under the node-wide check (verify_node_batch) and
-    the ranks' verdicts all-gathered: every rank returns the whole node's faulty rounds, ascending."""
+    the ranks' verdicts all-gathered: every rank returns the whole node's faulty rounds, ascending. exchange=True
+    runs every collective at world 1 too (_exchanges)."""
     import torch
     from .sync import NoBeaconStored  # noqa: F401  (the store error this mirrors)
 
@@ -313,9 +322,10 @@ def replay_shard(lib, scheme, pk, first, last, sig_of, rank, world, group=None, 
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     halo = None
-    if scheme.chained and world > 1:
+    xchg = _exchanges(world, exchange)
+    if scheme.chained and xchg:
         # only trailing ranks can be empty (shard_range gives the extra rounds to the lower ranks): they need no halo
-        halo = exchange_halo(sig_of.get(hi - 1) if hi > lo else None, rank, world, group)
+        halo = exchange_halo(sig_of.get(hi - 1) if hi > lo else None, rank, world, group, exchange)
     prev_first = prev_of_first if rank == 0 else halo
     if prev_first is MISSING_HALO:
         prev_first = None
@@ -367,7 +377,7 @@ def replay_shard(lib, scheme, pk, first, last, sig_of, rank, world, group=None, 
     try:
         verify_node_batch(lib, scheme, pk, d_rounds, d_sigs, n, d_verdict, None, partials, world, group,
                           d_prevs=d_prevs, prev_stride=stride, d_prev_lens=d_plen, seed=seed, rank=rank,
-                          stage_host=stage_host)
+                          stage_host=stage_host, exchange=exchange)
         v[dj] = d_verdict.cpu().numpy()[:n].astype(bool)
         if oversize:  # host digest + device pairing check (the scheme path routes long records that way)
             j = np.array(oversize, dtype=np.int64)
@@ -377,9 +387,9 @@ def replay_shard(lib, scheme, pk, first, last, sig_of, rank, world, group=None, 
         failed = str(e)
     v &= ~bad_len[:len(idx)]
     ok_range[np.array(idx, dtype=np.int64)] = v.astype(np.uint8)
-    bits = pack_bits(torch.from_numpy(ok_range).to(_collective_device(group) if world > 1 else torch.device("cpu")))
+    bits = pack_bits(torch.from_numpy(ok_range).to(_collective_device(group) if xchg else torch.device("cpu")))
     faulty = []
-    for r_, b_ in enumerate(gather_verdicts(bits, world, group, failed=failed)):
+    for r_, b_ in enumerate(gather_verdicts(bits, world, group, failed=failed, exchange=exchange)):
         a, z = shard_range(r_, world, last - first + 1)
         got = np.unpackbits(b_.cpu().numpy())[:z - a]
         faulty += [first + a + int(i) for i in np.flatnonzero(got == 0)]

@@ -252,7 +252,8 @@ def _free_port():
     return p
 
 
-def _replay_worker(rank, world, port, name, pk, first, last, local, genesis, q, stage_host=None):
+def _replay_worker(rank, world, port, name, pk, first, last, local, genesis, q, stage_host=None, backend="gloo",
+                   exchange=None):
     try:
         import torch
         import torch.distributed as dist
@@ -261,15 +262,18 @@ def _replay_worker(rank, world, port, name, pk, first, last, local, genesis, q, 
         from drand_amd.dist import replay_shard
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
         lib = _lib.load()
         assert lib.dh_init(1) == 0, _lib.last_error()
         torch.cuda.set_device(0)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         s = scheme_from_name(name)
         res = []
         for case_local in local:
             res.append(replay_shard(lib, s, pk, first, last, case_local, rank, world, prev_of_first=genesis, seed=0,
-                                    stage_host=stage_host))
+                                    stage_host=stage_host, exchange=exchange))
         q.put({"rank": rank, "faulty": res})
         dist.barrier()
         dist.destroy_process_group()
@@ -326,6 +330,59 @@ def test_replay_shard_two_processes(dh, oracle, stage_host):
     heads = [k + 1 for k in range(100, n, 100)]  # segment heads of the signer (see _chain)
     assert by_rank[0][2] == heads
     assert {hi0, hi0 + 1} <= set(by_rank[0][0]) and {hi0, hi0 + 1} <= set(by_rank[0][1])
+
+
+def test_replay_rccl_one_rank_group(dh, oracle):
+    """The RCCL branch on one GPU: dist.replay_shard in a spawned process over a one-rank `nccl` process group with
+    exchange=True, so the halo exchange, the all-gather of the partial record on the batch's library stream
+    (torch ExternalStream -> RCCL's stream -> dh_batch_check) and the verdict gather all run through RCCL, as on a
+    multi-GPU node (RCCL takes one rank per GPU, so two ranks cannot share this box's GPU). A chained chain with a
+    swapped and a missing record, and the clean chain: the faulty sets equal the serial oracle replay."""
+    import torch.multiprocessing as mp
+    s = dh.scheme_from_name(CHAINED)
+    n = 2000
+    sk, pk, sigs = _chain(s, n, every=250, seed=11)
+    store = {r + 1: sigs[r].tobytes() for r in range(n)}
+    store[0] = GENESIS
+    case_a = dict(store)
+    case_a[700] = store[699]
+    case_b = dict(store)
+    del case_b[1500]
+    cases = [case_a, case_b, store]
+    local = [{r: c[r] for r in range(1, n + 1) if r in c} for c in cases]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_replay_worker, args=(0, 1, _free_port(), CHAINED, pk, 1, n, local, GENESIS, q, False,
+                                                 "nccl", True))
+    p.start()
+    msg = q.get(timeout=240)
+    p.join(timeout=60)
+    assert "error" not in msg, msg.get("error")
+    assert p.exitcode == 0
+    for c, got in zip(cases, msg["faulty"]):
+        assert got == _oracle_replay(oracle, CHAINED, pk, c, 1, n)
+    assert {700, 701} <= set(msg["faulty"][0]) and {1500, 1501} <= set(msg["faulty"][1])
+    assert msg["faulty"][2] == [k + 1 for k in range(250, n, 250)]
+
+
+def test_bench_rccl_one_rank_group():
+    """bench.py --exchange always at N = 1: the node-wide batches of the multi-GPU bench (record all-gathered over RCCL
+    on each batch's stream, check queued after it, verdict bitmaps gathered) on a one-rank nccl group; every verdict
+    valid and the line names the RCCL all-gather."""
+    import subprocess
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--exchange", "always", "--node-check", "on",
+           "--rounds-per-gpu", "131072", "--steps", "4", "--warmup", "2", "--streams", "4", "--no-cpu-baseline",
+           "--roofline-steps", "0", "--single-call-steps", "0"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, out.stdout[-2000:]
+    res = json.loads(line[0])
+    assert res["n_gpus"] == 1 and res["verdicts_ok"] is True
+    assert "RCCL all-gather, one-rank group" in res["config"]["parallelism"]
 
 
 # ---------------------------------------------------------------- relay-s3 through the device
