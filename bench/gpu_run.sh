@@ -9,6 +9,7 @@
 #   bench[:<args>]         python bench.py <args>            -> gpurun_out/bench_<tag>_<i>.json
 #   config:<args>          python bench/bench_configs.py <args> -> gpurun_out/config_<tag>_<i>.json
 #   rocprof[:<args>]       rocprofv3 --kernel-trace --stats of python3 bench.py <args> -> gpurun_out/prof_<tag>_<i>/
+#   rocprofcfg:<args>      the same of python3 bench/bench_configs.py <args>        -> gpurun_out/prof_<tag>_<i>/
 #   pmc:<counters>[@<args>] one rocprofv3 --pmc pass of bench.py <args> -> gpurun_out/pmc_<tag>_<i>/
 #   py:<script args>       python <script args>              -> gpurun_out/py_<tag>_<i>.log
 #   env:<NAME>=<value>     export a variable for the steps after it (env:NAME= clears it)
@@ -48,6 +49,9 @@ for step in "$@"; do
       cut -c1-400 "$O/config_${T}_$i.json" ;;
     rocprof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_${T}_$i" -o run -- python3 bench.py $arg \
+        > "$O/prof_${T}_$i.json" 2> "$O/prof_${T}_$i.err" ;;
+    rocprofcfg)
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof_${T}_$i" -o run -- python3 bench/bench_configs.py $arg \
         > "$O/prof_${T}_$i.json" 2> "$O/prof_${T}_$i.err" ;;
     pmc)
       ctr=${arg%%@*}
