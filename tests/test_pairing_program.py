@@ -27,6 +27,15 @@ def test_pairing_program_valid_and_committed():
     text = g.emit(progs)
     with open(os.path.join(ROOT, "drand_amd", "csrc", "pairing_vm.hpp")) as f:
         assert f.read() == text, "csrc/pairing_vm.hpp is stale: rerun drand_amd/tools/gen_pairing_vm.py"
+    # k_vm.hip stages one 16-bit descriptor (kind | count << 8) per phase and finds a phase's first op record as the
+    # running sum of the counts: the emitted records must follow phase order and the descriptors fit 16 bits
+    import re
+    for tag in g.TAGS:
+        m = re.search(r"%s_PHASES\[\d*\]\s*=\s*\{([^}]*)\}" % tag, text)
+        v = [int(x.strip().rstrip("u"), 0) for x in m.group(1).split(",") if x.strip()]
+        desc, first = v[0::2], v[1::2]
+        assert first[0] == 0 and all(first[i + 1] == first[i] + (desc[i] >> 8) for i in range(len(desc) - 1)), tag
+        assert max(desc) < 1 << 16, tag
 
 
 def _vm_finish_model(terms):
