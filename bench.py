@@ -8,7 +8,9 @@ contiguous 1M-round range of the chain, so N GPUs verify N x 1M rounds per step;
 chain over the N GPUs instead (strong scaling, e.g. the north_star's 1M-round chain on 8 GPUs). One "step" = every
 rank verifies its rounds once (fresh CSPRNG seed); with N > 1 each batch runs under the node-wide check: the ranks'
 level-0 RLC sums are all-gathered over RCCL and ONE pairing check covers the node (drand_amd/dist.py), queued
-without a host wait; the verdict bitmaps are all-gathered at the end of the timed steps.
+without a host wait; the verdict bitmaps are all-gathered at the end of the timed steps. With N > 1 under weak scaling
+the line also carries "strong_scaling": the north_star's shape, ONE 1,048,576-round chain split over the N ranks
+(--strong-total-rounds), timed the same way after the weak leg.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--total-rounds n | --rounds-per-gpu n] [--scheme name]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -52,6 +54,9 @@ def parse():
                     help="strong scaling: one chain of this many rounds split over the GPUs")
     ap.add_argument("--rounds-per-gpu", type=int, default=0,
                     help="weak scaling: rounds per GPU (default 1048576 when --total-rounds is not given)")
+    ap.add_argument("--strong-total-rounds", type=int, default=1 << 20,
+                    help="N > 1, weak scaling: also time ONE chain of this many rounds split over the N ranks and report "
+                         "it as strong_scaling (0: skip)")
     ap.add_argument("--scheme", default="bls-unchained-g1-rfc9380")
     ap.add_argument("--cpu-sample-seconds", type=float, default=8.0,
                     help="wall time of the bounded CPU-baseline sample (after the GPU legs; kept short so the GPU work is "
@@ -192,37 +197,70 @@ def main():
     weak = args.total_rounds <= 0
     if weak:
         per_gpu = args.rounds_per_gpu or (1 << 20)
-        rounds = shard_rounds(rank, world, per_gpu)
         total = world * per_gpu
     else:
-        rounds = strong_shard(rank, world, args.total_rounds)
         total = args.total_rounds
-    n = len(rounds)
     sk = (int.from_bytes(hashlib.sha256(b"drandhip-sk-" + args.scheme.encode()).digest(), "big") % R_ORDER).to_bytes(32, "big")
     pk = sch.public_key(sk)
-    t0 = time.perf_counter()
-    sigs = sch.sign_beacons(sk, rounds)  # synthetic chain, signed on the GPU (not timed)
-    t_sign = time.perf_counter() - t0
-
-    d_rounds = torch.from_numpy(rounds.view(np.int64)).to(dev)
-    d_sigs = torch.from_numpy(sigs).to(dev)
     S = max(1, args.streams)
-    d_verdict = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(S)]
-    d_rand = [torch.zeros((n, 32), dtype=torch.uint8, device=dev) for _ in range(S)]
     pbytes = lib.dh_partial_bytes(sch.id)
-    d_part = [torch.zeros(pbytes, dtype=torch.uint8, device=dev) for _ in range(S)]
+
+    class Work:
+        """One rank's rounds resident in HBM, with 2 x S output slots: a slot's verdicts are packed (pack_bits, on
+        torch's stream) after its batch finished, and the slot is not handed to another batch before that packing has
+        run (its event; ADVICE r04: the next begin's memset on the library stream raced the packing). With 2 x S slots
+        the packing of a slot finished long before the slot comes round again, so the wait is a formality."""
+
+        def __init__(self, rnds):
+            self.rounds = rnds
+            self.n = len(rnds)
+            t0 = time.perf_counter()
+            self.sigs = sch.sign_beacons(sk, rnds)  # synthetic chain, signed on the GPU (not timed)
+            self.sign_s = time.perf_counter() - t0
+            self.d_rounds = torch.from_numpy(rnds.view(np.int64)).to(dev)
+            self.d_sigs = torch.from_numpy(self.sigs).to(dev)
+            self.d_verdict = [torch.zeros(self.n, dtype=torch.uint8, device=dev) for _ in range(2 * S)]
+            self.d_rand = [torch.zeros((self.n, 32), dtype=torch.uint8, device=dev) for _ in range(2 * S)]
+            self.d_part = [torch.zeros(pbytes, dtype=torch.uint8, device=dev) for _ in range(2 * S)]
+            self.packed = [None] * (2 * S)
+            self.used = set()
+
+        def take(self, slot):
+            ev = self.packed[slot]
+            if ev is not None:
+                ev.synchronize()
+            self.used.add(slot)
+            return slot
+
+        def pack(self, slot):
+            bits = pack_bits(self.d_verdict[slot])
+            ev = torch.cuda.Event()
+            ev.record()
+            self.packed[slot] = ev
+            return bits
+
+        def all_valid(self):
+            return all(bool(self.d_verdict[k].cpu().numpy().all()) for k in sorted(self.used))
+
+    if weak:
+        work = Work(shard_rounds(rank, world, per_gpu))
+    else:
+        work = Work(strong_shard(rank, world, args.total_rounds))
+    n = work.n
+    rounds, sigs, t_sign = work.rounds, work.sigs, work.sign_s
+    d_rounds, d_sigs = work.d_rounds, work.d_sigs
     torch.cuda.synchronize()
     state = {"node_check": node_check}
 
-    def verify(slot):
-        rc = lib.dh_verify_batch_device(sch.id, pk, len(pk), ctypes.c_void_p(d_rounds.data_ptr()),
-                                        ctypes.c_void_p(d_sigs.data_ptr()), sch.sig_len, None, 0, None, n,
-                                        ctypes.c_void_p(d_verdict[slot].data_ptr()),
-                                        ctypes.c_void_p(d_rand[slot].data_ptr()), 0, None, None)
+    def verify(wk, slot):
+        rc = lib.dh_verify_batch_device(sch.id, pk, len(pk), ctypes.c_void_p(wk.d_rounds.data_ptr()),
+                                        ctypes.c_void_p(wk.d_sigs.data_ptr()), sch.sig_len, None, 0, None, wk.n,
+                                        ctypes.c_void_p(wk.d_verdict[slot].data_ptr()),
+                                        ctypes.c_void_p(wk.d_rand[slot].data_ptr()), 0, None, None)
         if rc != 0:
             raise RuntimeError("dh_verify_batch_device: %s" % _lib.last_error())
 
-    def run_node_steps(k_steps, streams, gather=True):
+    def run_node_steps(wk, k_steps, streams, gather=True):
         """k_steps batches under the node-wide check, `streams` in flight, driven by ONE host thread: batch k is begun,
         its record all-gathered and its check queued (no host wait under nccl), and the oldest batch is finished once
         `streams` are queued. One thread issues every rank's collectives in the same order over one process group."""
@@ -235,7 +273,7 @@ def main():
             t0 = time.perf_counter()
             h.finish()
             t1 = time.perf_counter()
-            bits.append(pack_bits(d_verdict[slot]))
+            bits.append(wk.pack(slot))
             ht["finish_wait"] += t1 - t0
             ht["pack"] += time.perf_counter() - t1
             ht["batches"] += 1
@@ -243,15 +281,15 @@ def main():
         for k in range(k_steps):
             if len(pending) == streams:
                 retire()
-            slot = k % streams
+            slot = wk.take(k % (2 * streams))
             # the record, the collective and the check of a batch run on that batch's own library stream
             # (dist.begin_node_batch): no stream shared by the batches carries a wait for another batch's record (r04a
             # ordered them all through torch's current stream and chained every batch's per-round kernels behind the
             # previous batch's MSM: 14.2 M/s at 131k rounds, 8 slots)
             t0 = time.perf_counter()
-            pending.append((slot, begin_node_batch(lib, sch, pk, d_rounds, d_sigs, n, d_verdict[slot], d_rand[slot],
-                                                   d_part[slot], world, None, stage_host=gloo, rank=rank,
-                                                   inputs_ready=True, exchange=xchg)))
+            pending.append((slot, begin_node_batch(lib, sch, pk, wk.d_rounds, wk.d_sigs, wk.n, wk.d_verdict[slot],
+                                                   wk.d_rand[slot], wk.d_part[slot], world, None, stage_host=gloo,
+                                                   rank=rank, inputs_ready=True, exchange=xchg)))
             ht["begin_exchange_check"] += time.perf_counter() - t0
         while pending:
             retire()
@@ -261,19 +299,20 @@ def main():
             gather_verdicts(b.cpu() if gloo else b, world, exchange=xchg)
         torch.cuda.synchronize()
 
-    def run_steps(k_steps, streams, gather=True):
-        """k_steps batches, `streams` in flight: thread t runs steps t, t+streams, ... on its own output slot."""
+    def run_steps(wk, k_steps, streams, gather=True):
+        """k_steps batches, `streams` in flight: thread t runs steps t, t+streams, ... alternating over its two slots."""
         if state["node_check"]:
-            return run_node_steps(k_steps, streams, gather)
+            return run_node_steps(wk, k_steps, streams, gather)
         errs = []
         bits = [None] * k_steps
 
         def worker(t):
             try:
                 torch.cuda.set_device(dev_index)
-                for k in range(t, k_steps, streams):
-                    verify(t)
-                    bits[k] = pack_bits(d_verdict[t])
+                for j, k in enumerate(range(t, k_steps, streams)):
+                    slot = wk.take(2 * t + (j & 1))
+                    verify(wk, slot)
+                    bits[k] = wk.pack(slot)
             except Exception as e:  # surfaced below
                 errs.append(e)
 
@@ -289,6 +328,18 @@ def main():
             gather_verdicts(b.cpu() if gloo else b, world, exchange=xchg)
         torch.cuda.synchronize()
 
+    def timed(wk, k_steps):
+        """Barrier + synchronize on both sides of k_steps batches; the max over ranks of the wall time."""
+        if pg:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_steps(wk, k_steps, S)
+        torch.cuda.synchronize()
+        if pg:
+            dist.barrier()
+        return time.perf_counter() - t0
+
     def profile_read():
         buf = ctypes.create_string_buffer(1 << 16)
         lib.dh_profile_read(buf, len(buf))
@@ -296,44 +347,55 @@ def main():
 
     # warm-up: at least one batch per stream, so every library worker (stream + device workspace) exists before
     # the timed region; W < S would leave workspace allocation inside it
-    warm_batches = max(args.warmup, S) if args.warmup else 0
-    run_steps(warm_batches, S)
+    warm_batches = max(args.warmup, 2 * S) if args.warmup else 0
+    run_steps(work, warm_batches, S)
     lib.dh_profile(0 if args.no_stage_times else 1)
     state["node_host_s"] = collections.Counter()  # the timed region's host time per pipeline phase
-    if pg:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run_steps(args.steps, S)
-    torch.cuda.synchronize()
-    if pg:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(work, args.steps)
     prof = profile_read()
     # sanity (outside the timed region): every synthetic round verifies, randomness = SHA-256(sig)
-    ok = all(bool(d.cpu().numpy().all()) for d in d_verdict[:min(S, args.steps)])
-    r0 = d_rand[0].cpu().numpy()[0].tobytes()
+    ok = work.all_valid()
+    r0 = work.d_rand[min(work.used)].cpu().numpy()[0].tobytes()
     ok = ok and r0 == hashlib.sha256(sigs[0].tobytes()).digest()
+    node_host = dict(state.get("node_host_s", {}))
+
+    # The north_star's shape beside the weak-scaling value: ONE --strong-total-rounds chain (1M) split over the N
+    # ranks, each rank's shard under the node-wide check, timed the same way (after the weak leg, same workers).
+    strong = None
+    if weak and world > 1 and args.strong_total_rounds > 0:
+        swork = Work(strong_shard(rank, world, args.strong_total_rounds))
+        torch.cuda.synchronize()
+        run_steps(swork, 2 * S, S)
+        s_el = timed(swork, args.steps)
+        s_ok = swork.all_valid()
+        t = torch.tensor([s_el, 0.0 if s_ok else 1.0], dtype=torch.float64, device="cpu" if gloo else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        s_el, s_ok = float(t[0]), float(t[1]) == 0.0
+        strong = {"scaling": "strong", "rounds_total": args.strong_total_rounds, "rounds_per_gpu": swork.n,
+                  "steps": args.steps, "value": round(args.strong_total_rounds * args.steps / s_el, 1),
+                  "unit": "beacons/s", "ms_per_step": round(s_el * 1000.0 / args.steps, 3), "verdicts_ok": s_ok,
+                  "what": "one %d-round quicknet chain split over the %d ranks per step (node-wide RLC check), max-over-"
+                          "ranks wall time of the steps" % (args.strong_total_rounds, world)}
+        del swork
 
     # Roofline pass (after the timed region, not counted in `value`): with S batches in flight the kernels of
     # different batches share the CUs, so per-launch durations there are not one kernel's speed. Single-stream
     # local batches give each kernel the whole GPU; the dominant kernel's roofline comes from their HIP events (on
     # the library's stream). bench/profile.sh records the rocprofv3 kernel trace of the same batches.
-    node_host = dict(state.get("node_host_s", {}))
     state["node_check"] = False
     prof1 = {}
     if args.roofline_steps:
         lib.dh_profile(1)
-        run_steps(args.roofline_steps, 1, gather=False)
+        run_steps(work, args.roofline_steps, 1, gather=False)
         prof1 = profile_read()
         lib.dh_profile(0)
     single = None
     if args.single_call_steps and world == 1:  # the drop-in shape: ONE call at a time, split internally
         chunk, workers = (int(x) for x in args.single_call_split.split(","))
         lib.dh_set_split(chunk, workers)
-        run_steps(1, 1, gather=False)  # warm the split workers
+        run_steps(work, 1, 1, gather=False)  # warm the split workers
         t1 = time.perf_counter()
-        run_steps(args.single_call_steps, 1, gather=False)
+        run_steps(work, args.single_call_steps, 1, gather=False)
         dt = time.perf_counter() - t1
         single = {"value": round(n * args.single_call_steps / dt, 1), "unit": "beacons/s",
                   "ms_per_call": round(dt * 1000 / args.single_call_steps, 3),
@@ -422,6 +484,7 @@ def main():
         "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in prof.items()},
         "stages_ms_single_stream": {k: round(v["total_ms"] / max(1, v["count"]), 3) for k, v in prof1.items()},
         "single_call": single,
+        "strong_scaling": strong,
         "node_host_ms_per_batch": ({k: round(v * 1000 / node_host["batches"], 3) for k, v in node_host.items()
                                     if k != "batches"} if node_host.get("batches") else None),
         "sign_seconds": round(t_sign, 2),

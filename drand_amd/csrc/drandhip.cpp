@@ -25,6 +25,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -93,6 +94,8 @@ struct worker {
   // stream), and the gathered records are complete on the caller's stream (the tail waits for it)
   hipEvent_t part_ready = nullptr, gath_ready = nullptr;
   bool busy = false;
+  // leased by a node batch (dh_batch_begin until dh_batch_finish): held across calls, released only by the caller
+  bool node_held = false;
   // per-round state
   dbuf status, sig_aff, q_pts, scal, entries, verdict_tmp, rand_tmp, h2c_tmp;
   // the MSM's 28-bit points (launch_msm_prep28, G1): sigma and its phi image (32 words each), hash points (48 words)
@@ -182,9 +185,22 @@ int ensure_init_locked(uint32_t mask) {
   return DH_OK;
 }
 
+// How long a blocking call waits for a worker while EVERY worker is held by an unfinished node batch (those are
+// released only by their callers' dh_batch_finish, possibly on the waiting thread itself): then DH_EBUSY, not a
+// deadlock. DRANDHIP_LEASE_TIMEOUT_MS overrides (default 30 s).
+static std::chrono::milliseconds node_held_timeout() {
+  static const long v = [] {
+    const char* e = getenv("DRANDHIP_LEASE_TIMEOUT_MS");
+    const long x = e ? atol(e) : 0;
+    return x > 0 ? x : 30000L;
+  }();
+  return std::chrono::milliseconds(v);
+}
+
 // A worker for the duration of a call. The pool holds at most g_ctx.max_workers: a blocking call waits for an idle
 // one; wait = false (dh_batch_begin, whose lease spans a collective with the other ranks, so waiting could deadlock
-// the node) fails with DH_EBUSY instead.
+// the node) fails with DH_EBUSY instead, and its worker is marked node_held until dh_batch_finish. A blocking call
+// that finds every worker node_held waits at most node_held_timeout() and then fails with DH_EBUSY.
 struct lease {
   worker* w = nullptr;
   int rc = DH_OK;
@@ -208,14 +224,24 @@ struct lease {
         rc = fail(DH_EBUSY, "all %zu library workers are busy (DRANDHIP_MAX_WORKERS)", g_ctx.max_workers);
         return;
       }
-      g_ctx.freed.wait(lk);
+      const bool all_node_held =
+          std::all_of(g_ctx.pool.begin(), g_ctx.pool.end(), [](const worker* x) { return x->node_held; });
+      if (!all_node_held) {
+        g_ctx.freed.wait(lk);
+      } else if (g_ctx.freed.wait_for(lk, node_held_timeout()) == std::cv_status::timeout) {
+        rc = fail(DH_EBUSY, "all %zu library workers are held by unfinished node batches (dh_batch_finish them first)",
+                  g_ctx.max_workers);
+        return;
+      }
     }
     w->busy = true;
+    w->node_held = !wait;
   }
   ~lease() {
     if (!w) return;
     std::lock_guard<std::mutex> lk(g_ctx.mu);
     w->busy = false;
+    w->node_held = false;
     g_ctx.freed.notify_all();
     auto it = std::find(g_ctx.retired.begin(), g_ctx.retired.end(), w);
     if (it != g_ctx.retired.end()) {  // dh_shutdown ran during this call
@@ -1552,8 +1578,11 @@ int dh_batch_check(dh_batch* b, const uint8_t* d_partials, size_t k, void* hip_s
   }
   int rc = queue_node_check(w, g2, b->pk.data(), b->pk.size(), d_partials, k, bs);
   if (rc) return rc;
-  // passed: every decoded round of this batch is valid, marked on the device
-  HIP_TRY(dh::launch_node_mark(b->n, w->node_res.as<uint8_t>(), w->status.as<uint8_t>(), b->d_verdict, bs));
+  // passed: every decoded round of this batch is valid, marked on the device. A one-round batch put only the
+  // identity into the node-wide sums (verify_core VM_BEGIN, n < 2), so the check says nothing about its round: it is
+  // not marked here, and dh_batch_finish always gives it its leaf check.
+  if (b->n >= 2)
+    HIP_TRY(dh::launch_node_mark(b->n, w->node_res.as<uint8_t>(), w->status.as<uint8_t>(), b->d_verdict, bs));
   b->checked = true;
   return DH_OK;
 }
@@ -1596,8 +1625,9 @@ int dh_batch_finish(dh_batch* b, int node_pass, uint64_t stats_out[4]) {
       rc = fail(DH_EABANDONED, "node batch abandoned: dh_batch_begin failed on another rank");
     } else {
       ret = res == 1 ? 1 : 0;
-      // passed: the verdicts are already marked (dh_batch_check); the level bookkeeping only when stats are asked
-      if (res != 1 || stats_out)
+      // passed: the verdicts are already marked (dh_batch_check); the level bookkeeping only when stats are asked.
+      // A one-round batch is never covered by the node check: its leaf check runs in every case.
+      if (res != 1 || stats_out || b->n < 2)
         rc = verify_core(w, b->scheme, b->pk.data(), b->pk.size(), b->d_rounds, b->d_sigs, b->sig_stride, b->d_prevs,
                          b->prev_stride, b->d_prev_lens, b->n, b->d_verdict, b->d_rand, 0, b->st, stats_out, nullptr,
                          res == 1 ? VM_FINISH_PASS : VM_FINISH);

@@ -36,7 +36,8 @@ extern "C" {
 #define DH_ENOMEM (-3)   /* device allocation failed */
 #define DH_EKEY (-4)     /* the group public key does not decode to a subgroup point */
 #define DH_ERECOVER (-5) /* Recover: fewer than t valid partial signatures */
-#define DH_EBUSY (-6)    /* dh_batch_begin: every library worker is held (DRANDHIP_MAX_WORKERS, default 24) */
+#define DH_EBUSY (-6)    /* every library worker is held (DRANDHIP_MAX_WORKERS, default 24): dh_batch_begin at once,
+                            a blocking call after DRANDHIP_LEASE_TIMEOUT_MS when node batches hold them all */
 #define DH_EABANDONED (-7) /* node-wide batch: some rank's dh_batch_begin failed, every rank abandons the batch */
 
 /* scheme ids, in the order of crypto/schemes.go:206-219 plus the RFC 9380 quicknet scheme */
@@ -178,7 +179,10 @@ int dh_verify_partials_batch(int scheme, const uint8_t* commits, int t, int n_no
  *
  * A batch holds one library worker from begin to finish (DH_EBUSY if none is idle: begin never waits, since the
  * other ranks may be waiting in the collective); the arguments of dh_batch_begin must stay valid until
- * dh_batch_finish returns. dh_batch_finish with node_pass 1 / 0 (a result the caller obtained itself, e.g. from
+ * dh_batch_finish returns. A blocking call (any other entry point) made while EVERY worker is held by unfinished
+ * batches waits at most DRANDHIP_LEASE_TIMEOUT_MS (default 30 s) for one and then fails with DH_EBUSY: finish the
+ * batches first. A batch of one round contributes the identity to the node-wide sums, so its round always gets its
+ * own check in dh_batch_finish, whatever the node-wide result. dh_batch_finish with node_pass 1 / 0 (a result the caller obtained itself, e.g. from
  * dh_check_partials) accepts every decoded round / runs the shard's own check and returns DH_OK; node_pass < 0
  * (other than DH_NODE_CHECKED) abandons the batch. dh_check_partials is the standalone check of k records (it
  * leases its own worker and blocks): pass_out = 1 / 0, DH_EABANDONED when a status word is nonzero.

@@ -115,7 +115,7 @@ def test_node_wide_check_all_schemes(dh, oracle, name, mode):
     pb = lib.dh_partial_bytes(s.id)
     assert pb == 2 * (72 if s.sig_len == 96 else 36) * 4 + 16
 
-    def run(sig_arr, seed):
+    def run(sig_arr, seed, with_stats=True):
         prev = np.zeros((n, 96), np.uint8)
         plen = np.full(n, 96, np.uint32)
         if s.chained:  # the stored column: prev of round k = stored sig of k-1 (halo across shards included)
@@ -159,7 +159,7 @@ def test_node_wide_check_all_schemes(dh, oracle, name, mode):
                 assert lib.dh_batch_check(b, ctypes.c_void_p(parts.data_ptr()), len(shards), sp) == 0, _lib.last_error()
             for b in handles:
                 st = (ctypes.c_uint64 * 4)()
-                r = lib.dh_batch_finish(b, _lib.DH_NODE_CHECKED, st)
+                r = lib.dh_batch_finish(b, _lib.DH_NODE_CHECKED, st if with_stats else None)
                 assert r in (0, 1), _lib.last_error()
                 results.append(r)
                 stats.append(list(st))
@@ -201,6 +201,18 @@ def test_node_wide_check_all_schemes(dh, oracle, name, mode):
     ref, _ = s.verify_beacons(pk, rounds, bad, [p for p in ([GENESIS] + [x.tobytes() for x in bad[:-1]])]
                               if s.chained else None, seed=5)
     assert np.array_equal(ref, v)
+    if mode == "device":
+        # only the one-round shard is bad, finished without stats (NodeBatch.finish()): its identity record lets the
+        # node check pass on the other shards' sums (unchained schemes), and the round must still get its own check
+        # (it used to be marked valid by the node check)
+        lone = sigs.copy()
+        lone[b0 - 1] = lone[b0 + 3]
+        ok, v, _ = run(lone, 9, with_stats=False)
+        sig_of = {r + 1: lone[r].tobytes() for r in range(n)}
+        sig_of[0] = GENESIS
+        want = _oracle_replay(oracle, name, pk, sig_of, 1, n)
+        assert [int(r) + 1 for r in np.flatnonzero(~v)] == want
+        assert b0 in want and ok == (0 if s.chained else 1)
 
 
 def test_node_batch_abandoned(dh):
@@ -417,20 +429,29 @@ def test_relay_s3_sync_device(dh, oracle):
 def test_bench_launches_ranks():
     """`python bench.py --gpus 2` with no launcher spawns the two ranks itself (torch.distributed.run in a child
     process, before any HIP call) and prints rank 0's line: n_gpus 2, the node-wide check as the parallelism, every
-    verdict valid. gloo rehearsal: both ranks on GPU 0, strong scaling of a 262,144-round chain."""
+    verdict valid. gloo rehearsal: both ranks on GPU 0, strong scaling of a 262,144-round chain; then weak scaling,
+    whose line also carries the strong_scaling field (one chain split over the ranks, the north_star's shape)."""
     import subprocess
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--total-rounds", "262144",
-           "--steps", "2", "--warmup", "1", "--streams", "4", "--no-cpu-baseline", "--roofline-steps", "0",
-           "--single-call-steps", "0"]
-    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "2",
+            "--warmup", "1", "--streams", "4", "--no-cpu-baseline", "--roofline-steps", "0", "--single-call-steps", "0"]
+    out = subprocess.run(base + ["--total-rounds", "262144"], env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     line = [x for x in out.stdout.splitlines() if x.startswith("{")]
     assert len(line) == 1, out.stdout[-2000:]
     res = json.loads(line[0])
     assert res["n_gpus"] == 2 and res["verdicts_ok"] is True and res["scaling"] == "strong"
     assert "node-wide RLC check" in res["config"]["parallelism"] and res["config"]["rounds_per_gpu"] == 131072
+    assert res["strong_scaling"] is None  # the value itself is the strong figure
+    out = subprocess.run(base + ["--rounds-per-gpu", "65536", "--strong-total-rounds", "131072"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][0])
+    assert res["scaling"] == "weak" and res["verdicts_ok"] is True and res["config"]["rounds_total"] == 131072
+    st = res["strong_scaling"]
+    assert st["scaling"] == "strong" and st["rounds_total"] == 131072 and st["rounds_per_gpu"] == 65536
+    assert st["verdicts_ok"] is True and st["value"] > 0
     # under a launcher WORLD_SIZE must match --gpus
     bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True, text=True,
                          env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), timeout=120)

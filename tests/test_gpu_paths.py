@@ -646,3 +646,84 @@ def test_threshold_scheme_dropin_shapes(dh, oracle, scheme):
     with pytest.raises(SchemeError, match="not enough good public shares"):
         ts.recover(commits, msgs[0], [other, part[1], part[2], part[11], part[5][:-1]], t, n)
     assert oracle.recover(s.name, commits, t, n, msgs[0], [other, part[1], part[2], part[11]]) is None
+
+
+# ---------------------------------------------------------------- the Go batch methods' C calls, buffer by buffer
+def test_go_batch_call_shapes(dh, oracle):
+    """The exact C calls of INTEGRATION.md §2.4 against the oracle. Scheme.VerifyBeacons: dh_verify_batch over host
+    buffers built as the Go code builds them — a chained window whose previous signatures have the lengths a trimmed
+    store yields (the 32-byte genesis seed, 96-byte signatures, an empty and a 100-byte corrupted record), packed at
+    stride = max(4, the longest rounded up to 4) with a u32 length per round, and a wrong-length signature replaced by
+    an all-zero record (kyber rejects it); verdict bytes only (rand_out NULL, seed 0). RecoverBatch: dh_recover_batch
+    with the wrong-length partial records dropped, the messages back to back, u32 offsets per round and one zero
+    record of padding. Each verdict / recovered signature equals the oracle's (kyber restated)."""
+    import ctypes
+    import chainsynth
+    from drand_amd import _lib
+    lib = _lib.load()
+    s = dh.scheme_from_name(CHAINED)
+    sk = _secret(b"go-shapes")
+    pk = s.public_key(sk)
+    n = 40
+    genesis = hashlib.sha256(b"drandhip-genesis").digest()
+    sigs = chainsynth.sign_chain(s, sk, 1, n, genesis, [], np.random.default_rng(2))
+    recs = [(r + 1, sigs[r].tobytes(), genesis if r == 0 else sigs[r - 1].tobytes()) for r in range(n)]
+    recs[7] = (8, recs[7][1], b"")                           # empty previous record
+    recs[12] = (13, recs[12][1], bytes(range(100)))          # corrupted 100-byte record
+    recs[20] = (21, recs[20][1][:-1], recs[20][2])           # wrong-length signature
+    recs[30] = (31, recs[31][1], recs[30][2])                # another round's signature
+    stride = 4
+    for _, _, p in recs:
+        stride = max(stride, (len(p) + 3) & ~3)
+    rounds = np.array([r for r, _, _ in recs], dtype=np.uint64)
+    sbuf = np.zeros((n, 96), np.uint8)
+    pbuf = np.zeros((n, stride), np.uint8)
+    plen = np.zeros(n, np.uint32)
+    for i, (_, sg, p) in enumerate(recs):
+        if len(sg) == 96:
+            sbuf[i] = np.frombuffer(sg, np.uint8)
+        pbuf[i, :len(p)] = np.frombuffer(p, np.uint8)
+        plen[i] = len(p)
+    verdict = np.zeros(n, np.uint8)
+    rc = lib.dh_verify_batch(s.id, pk, len(pk), rounds.ctypes.data, sbuf.ctypes.data, 96, pbuf.ctypes.data, stride,
+                             plen.ctypes.data, n, verdict.ctypes.data, None, 0)
+    assert rc == 0, _lib.last_error()
+    want = [len(sg) == 96 and oracle.verify_beacon(CHAINED, pk, r, sg, p) for r, sg, p in recs]
+    assert verdict.astype(bool).tolist() == want
+    assert [i + 1 for i in range(n) if not want[i]] == [8, 13, 21, 31]
+    # RecoverBatch
+    name = "pedersen-bls-unchained"
+    u = dh.scheme_from_name(name)
+    t, nn, nr = 5, 9, 6
+    coeffs, commits = _dealer(u, t, b"go-recover")
+    rr = np.arange(50, 50 + nr, dtype=np.uint64)
+    shares = {i: u.sign_beacons(_share(coeffs, i), rr) for i in range(nn)}
+    msgs = [u.digest_beacon(int(r)) for r in rr]
+    parts = []
+    for j in range(nr):
+        ps = [i.to_bytes(2, "big") + shares[i][j].tobytes() for i in ((j + k) % nn for k in range(t + 1))]
+        if j == 2:
+            ps.insert(0, ps[1][:-4])                         # wrong length: dropped before the call
+        if j == 4:
+            ps = ps[:t - 1] + [ps[t][:50]]                   # t - 1 well-sized: not enough good shares
+        parts.append(ps)
+    rec = 98
+    raw, off = b"", [0]
+    for ps in parts:
+        raw += b"".join(p for p in ps if len(p) == rec)
+        off.append(len(raw) // rec)
+    raw += bytes(rec)
+    offa = np.array(off, dtype=np.uint32)
+    rawa = np.frombuffer(raw, np.uint8).copy()
+    ma = np.frombuffer(b"".join(msgs), np.uint8).copy()
+    out = np.zeros((nr, 96), np.uint8)
+    st = np.zeros(nr, np.uint8)
+    rc = lib.dh_recover_batch(u.id, b"".join(commits), t, nn, ma.ctypes.data, rawa.ctypes.data, offa.ctypes.data, nr,
+                              out.ctypes.data, st.ctypes.data)
+    assert rc == 0, _lib.last_error()
+    for j in range(nr):
+        w = oracle.recover(name, commits, t, nn, msgs[j], [p for p in parts[j] if len(p) == rec])
+        assert (w is not None) == (st[j] == 1), j
+        if w is not None:
+            assert out[j].tobytes() == w, j
+    assert st.tolist() == [1, 1, 1, 1, 0, 1]

@@ -42,3 +42,26 @@ def test_corrupted_rounds_and_expected_set():
     assert np.array_equal(bad, chainsynth.corrupted_rounds(1 << 20, 1000))  # seeded
     exp = chainsynth.expected_faulty(np.array([0, 5, 6, 9]), 10)
     assert exp.tolist() == [0, 1, 5, 6, 7, 9]
+
+
+def test_g1_codec_round_trip_and_classes(oracle):
+    """The G1 variant (bench/g1_synth.py) used by the quicknet config-size GPU test."""
+    import g1_synth
+    name = "bls-unchained-g1-rfc9380"
+    c = json.load(open(os.path.join(GOLD, "chains.json")))[name]
+    rng = random.Random(6)
+    pk = bytes.fromhex(c["pk"])
+    for r, sig_hex in list(zip(c["rounds"], c["sigs"]))[:4]:
+        sig = bytes.fromhex(sig_hex)
+        assert g1_synth.compress(g1_synth.decompress(sig)) == sig
+        moved = g1_synth.plus_generator(sig)
+        assert oracle.decode(False, moved) == 1  # a valid subgroup point ...
+        assert not oracle.verify_beacon(name, pk, r, moved)  # ... not the signature
+        assert oracle.verify_beacon(name, pk, r, sig)
+        flipped = g1_synth.flip_bit(sig, rng)
+        assert sum(bin(a ^ b).count("1") for a, b in zip(flipped, sig)) == 1
+        assert not oracle.verify_beacon(name, pk, r, flipped)
+    for _ in range(3):
+        off = g1_synth.off_subgroup(rng)
+        assert g1_synth.compress(g1_synth.decompress(off)) == off  # on E1 ...
+        assert oracle.decode(False, off) != 1  # ... but rejected by the subgroup check
