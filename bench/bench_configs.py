@@ -292,7 +292,9 @@ def cfg_recover(args):
     cdt = time.perf_counter() - t0
     wm = workmodel()
     dev_ms = sum(x["total_ms"] for x in prof.values())
-    units = {"k_lagrange": wm["kernel_units_M_per_round"].get("k_lagrange_t33", 97700),
+    ku = wm["kernel_units_M_per_round"]
+    lag = ku.get("k_lagrange_t33_random", ku.get("k_lagrange_t33")) if args.subsets == "random" else ku.get("k_lagrange_t33")
+    units = {"k_lagrange": lag or 97700,
              "k_prep_sig<fp2>(partials)": wm["kernel_units_M_per_round"]["k_prep_sig<fp2>"]}
     roof = None
     if "k_lagrange" in prof and "k_prep_sig<fp2>(partials)" in prof:

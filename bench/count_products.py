@@ -88,21 +88,26 @@ def main():
     commits = [s.public_key(c.to_bytes(32, "big")) for c in coeffs]
     rounds = np.arange(1, nr + 1, dtype=np.uint64)
     shares = []
-    for i in range(t):
+    for i in range(n_nodes):
         x, acc = i + 1, 0
         for c in reversed(coeffs):
             acc = (acc * x + c) % R_ORDER
         shares.append(s.sign_beacons(acc.to_bytes(32, "big"), rounds))
     msgs = [s.digest_beacon(int(r)) for r in rounds]
-    parts = [[i.to_bytes(2, "big") + shares[i][j].tobytes() for i in range(t)] for j in range(nr)]
-    lib.dh_profile(1)
-    sigs, ok = s.recover_batch(commits, t, n_nodes, msgs, parts)
-    p = prof()
-    lib.dh_profile(0)
-    assert ok.all()
-    key = "tbls-recover-n64-t33/%d" % nr
-    out["per_round"][key] = {k: round(v["products"] / nr, 2) for k, v in p.items()}
-    print(key, out["per_round"][key], flush=True)
+    rng = np.random.default_rng(5)
+    # "first": signers 0 .. t-1 every round (configs[3]'s default); "random": a random t-subset per round (its variant:
+    # every round its own Lagrange basis, the regular-window chains)
+    for mode in ("first", "random"):
+        ids = [list(range(t)) if mode == "first" else list(rng.permutation(n_nodes)[:t]) for _ in range(nr)]
+        parts = [[int(i).to_bytes(2, "big") + shares[i][j].tobytes() for i in ids[j]] for j in range(nr)]
+        lib.dh_profile(1)
+        sigs, ok = s.recover_batch(commits, t, n_nodes, msgs, parts)
+        p = prof()
+        lib.dh_profile(0)
+        assert ok.all()
+        key = "tbls-recover-n64-t33%s/%d" % ("" if mode == "first" else "-random", nr)
+        out["per_round"][key] = {k: round(v["products"] / nr, 2) for k, v in p.items()}
+        print(key, out["per_round"][key], flush=True)
     line = json.dumps(out)
     if args.out:
         with open(args.out, "w") as f:

@@ -11,6 +11,7 @@
 #   rocprof[:<args>]       rocprofv3 --kernel-trace --stats of python3 bench.py <args> -> gpurun_out/prof_<tag>_<i>/
 #   rocprofcfg:<args>      the same of python3 bench/bench_configs.py <args>        -> gpurun_out/prof_<tag>_<i>/
 #   pmc:<counters>[@<args>] one rocprofv3 --pmc pass of bench.py <args> -> gpurun_out/pmc_<tag>_<i>/
+#   pmccfg:<counters>@<args> one rocprofv3 --pmc pass of bench/bench_configs.py <args> -> gpurun_out/pmc_<tag>_<i>/
 #   py:<script args>       python <script args>              -> gpurun_out/py_<tag>_<i>.log
 #   env:<NAME>=<value>     export a variable for the steps after it (env:NAME= clears it)
 #   sh:<script args>       bash <script args> (bench/pmc.sh, bench/bisect_sweep.sh: they time-limit their own steps)
@@ -58,6 +59,12 @@ for step in "$@"; do
       bargs=""
       [[ "$arg" == *@* ]] && bargs=${arg#*@}
       timeout -s KILL 300 rocprofv3 --pmc $ctr -d "$O/pmc_${T}_$i" -o run -- python3 bench.py $bargs \
+        > "$O/pmc_${T}_$i.json" 2> "$O/pmc_${T}_$i.err" ;;
+    pmccfg)
+      ctr=${arg%%@*}
+      cargs=""
+      [[ "$arg" == *@* ]] && cargs=${arg#*@}
+      timeout -s KILL 300 rocprofv3 --pmc $ctr -d "$O/pmc_${T}_$i" -o run -- python3 bench/bench_configs.py $cargs \
         > "$O/pmc_${T}_$i.json" 2> "$O/pmc_${T}_$i.err" ;;
     py)
       timeout -k 10 600 python $arg > "$O/py_${T}_$i.log" 2>&1

@@ -27,7 +27,8 @@ def main():
 
     q = pick("bls-unchained-g1-rfc9380", 1048576)
     u = pick("pedersen-bls-unchained", 1048576)
-    rec = next(v for k, v in counts.items() if k.startswith("tbls-recover"))
+    rec = next(v for k, v in counts.items() if k.startswith("tbls-recover-n64-t33/"))
+    rec_r = next((v for k, v in counts.items() if k.startswith("tbls-recover-n64-t33-random/")), None)
     units = {
         "k_prep_sig<fp>": q["k_prep_sig<fp>"],
         "k_prep_msg<fp>": q["k_prep_msg<fp>"],
@@ -37,6 +38,10 @@ def main():
         "msm_level0<fp2>": u["msm_level0"] + u.get("k_msm_prep28<fp2>", 0.0),
         "k_lagrange_t33": rec["k_lagrange"],
     }
+    if rec_r is not None:  # random signer subsets: every round its own basis, the regular-window chains
+        units["k_lagrange_t33_random"] = rec_r["k_lagrange"]
+        units["k_wnaf_table_t33_random"] = rec_r.get("k_wnaf_table", 0.0)
+    units["k_wnaf_table_t33"] = rec.get("k_wnaf_table", 0.0)
     wm["kernel_units_M_per_round"] = {k: round(v, 1) for k, v in units.items()}
     wm["executed_M_per_beacon"] = {
         "g1_sig": round(units["k_prep_sig<fp>"] + units["k_prep_msg<fp>"] + units["msm_level0"], 1),

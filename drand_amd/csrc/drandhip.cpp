@@ -115,7 +115,7 @@ struct worker {
   // tbls Recover
   dbuf r_commits, r_cstatus, r_caff, r_shares, r_raw, r_psigs, r_pidx, r_pstatus, r_paff, r_msgs, r_q, r_scal,
       r_round_of, r_e_pidx, r_e_sidx, r_e_grp, r_P, r_Q, r_f, r_skip, r_ok, r_sel, r_lam, r_lamset, r_rok, r_sig,
-      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_zs, r_tbl, r_rstat, r_ltmp, r_own;
+      r_sigbytes, r_status2, r_aff2, r_entries2, r_off, r_key, r_den, r_zs, r_tbl, r_rstat, r_ltmp, r_own, r_need;
   std::vector<uint8_t> h_verdict;
   // Recover: the (scheme, t, n_nodes, commits) whose decoded commits and public shares r_caff / r_shares hold
   std::vector<uint8_t> r_pub_key;
@@ -135,7 +135,7 @@ struct worker {
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
                    &r_raw, &r_psigs, &r_pidx, &r_pstatus, &r_paff, &r_msgs, &r_q, &r_scal, &r_round_of, &r_e_pidx,
                    &r_e_sidx, &r_e_grp, &r_P, &r_Q, &r_f, &r_skip, &r_ok, &r_sel, &r_lam, &r_lamset, &r_rok, &r_sig,
-                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_zs, &r_tbl, &r_rstat, &r_ltmp, &r_own, &node_sum, &node_res};
+                   &r_sigbytes, &r_status2, &r_aff2, &r_entries2, &r_off, &r_key, &r_den, &r_zs, &r_tbl, &r_rstat, &r_ltmp, &r_own, &r_need, &node_sum, &node_res};
     for (dbuf* b : all) b->release();
     if (stream) (void)hipStreamDestroy(stream);
     if (tail) (void)hipStreamDestroy(tail);
@@ -551,10 +551,28 @@ static bool lane_pairing() {
 }
 
 // key_h: [h_eff] pk next to a decoded G2 key (k_decode_key), or null (the check clears B's cofactor itself)
+// G2-signature group checks of up to this many groups clear B's cofactor inside the pairing program (NP2C: the
+// clearing's doublings spread over the lanes) instead of on one lane before it; DRANDHIP_NP2C=0 turns it off. Above
+// it the one-lane clearing wins: every group's lane runs in parallel, the NP2C workgroups queue for the CUs.
+static size_t np2c_max_groups() {
+  static const size_t v = [] {
+    const char* e = getenv("DRANDHIP_NP2C");
+    return e && e[0] == '0' ? (size_t)0 : (size_t)4096;
+  }();
+  return v;
+}
+
 static hipError_t group_check(worker* w, bool g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key,
                               uint8_t* pass, hipStream_t st, const uint32_t* key_h = nullptr) {
   if (lane_pairing()) return dh::launch_group_check(g2, A, B, ngroups, key, pass, st);
   hipError_t e;
+  if (g2 && ngroups <= np2c_max_groups()) {
+    if ((e = w->vm_pairs.ensure(ngroups * dh::group_check_c_pair_words() * 4)) != hipSuccess) return e;
+    if ((e = w->vm_live.ensure(ngroups * 3)) != hipSuccess) return e;
+    if ((e = w->vm_done.ensure(ngroups)) != hipSuccess) return e;
+    return dh::launch_group_check_vm_c(A, B, ngroups, key, w->vm_pairs.as<uint32_t>(), w->vm_live.as<uint8_t>(),
+                                       w->vm_done.as<uint8_t>(), pass, st);
+  }
   if ((e = w->vm_pairs.ensure(ngroups * 2 * 72 * 4)) != hipSuccess) return e;
   if ((e = w->vm_live.ensure(ngroups * 2)) != hipSuccess) return e;
   return dh::launch_group_check_vm(g2, A, B, ngroups, key, g2 ? nullptr : key_h, w->vm_pairs.as<uint32_t>(),
@@ -1138,11 +1156,14 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     if (own) entries = 8;
   }
   // 13. interpolation on the device
-  if (g2) {  // the partials' points in the 28-bit form, and their width-4 NAF tables, once per valid partial
+  if (g2) {  // the selected partials' points in the 28-bit form and their tables of odd multiples, once per partial
     HIP_TRY(w->r_zs.ensure(dh::wnaf_table_scratch_bytes(np, entries) + 256));
     HIP_TRY(w->r_tbl.ensure(np * (size_t)entries * 64 * 4 + 1024));
+    HIP_TRY(w->r_need.ensure(np + 4));
+    HIP_TRY(dh::launch_mark_selected(w->r_sel.as<uint32_t>(), w->r_rok.as<uint8_t>(), t, n_rounds, np, w->r_need.as<uint8_t>(),
+                                     st));
     HIP_TRY(T.run("k_wnaf_table", [&] {
-      return dh::launch_wnaf_table_g2(w->r_paff.as<uint32_t>(), w->r_ok.as<uint8_t>(), np, entries, w->r_tbl.as<uint32_t>(),
+      return dh::launch_wnaf_table_g2(w->r_paff.as<uint32_t>(), w->r_need.as<uint8_t>(), np, entries, w->r_tbl.as<uint32_t>(),
                                       w->r_zs.as<uint32_t>(), st);
     }));
   }
@@ -1578,11 +1599,10 @@ int dh_batch_check(dh_batch* b, const uint8_t* d_partials, size_t k, void* hip_s
   }
   int rc = queue_node_check(w, g2, b->pk.data(), b->pk.size(), d_partials, k, bs);
   if (rc) return rc;
-  // passed: every decoded round of this batch is valid, marked on the device. A one-round batch put only the
-  // identity into the node-wide sums (verify_core VM_BEGIN, n < 2), so the check says nothing about its round: it is
-  // not marked here, and dh_batch_finish always gives it its leaf check.
-  if (b->n >= 2)
-    HIP_TRY(dh::launch_node_mark(b->n, w->node_res.as<uint8_t>(), w->status.as<uint8_t>(), b->d_verdict, bs));
+  // the node-wide result (node_res[2]) and, when it passed, every decoded round of this batch marked valid on the
+  // device. A one-round batch put only the identity into the node-wide sums (verify_core VM_BEGIN, n < 2), so the check
+  // says nothing about its round: none is marked here, and dh_batch_finish always gives it its leaf check.
+  HIP_TRY(dh::launch_node_mark(b->n >= 2 ? b->n : 0, w->node_res.as<uint8_t>(), w->status.as<uint8_t>(), b->d_verdict, bs));
   b->checked = true;
   return DH_OK;
 }

@@ -368,6 +368,22 @@ __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restric
     }
   }
 }
+// need[e] = 1 for the partials some recovered round selected (sel, t per round): the tables are built for those only
+// (with more than t partials per round, every valid partial got a table that no round reads)
+__global__ void k_mark_selected(const uint32_t* __restrict__ sel, const uint8_t* __restrict__ rok, int t, size_t n_rounds,
+                                uint8_t* __restrict__ need) {
+  const size_t i = gtid();
+  if (i >= n_rounds * (size_t)t) return;
+  if (rok[i / t]) need[sel[i]] = 1;
+}
+hipError_t launch_mark_selected(const uint32_t* sel, const uint8_t* rok, int t, size_t n_rounds, size_t np, uint8_t* need,
+                                hipStream_t st) {
+  hipError_t e = hipMemsetAsync(need, 0, np, st);
+  if (e != hipSuccess || !n_rounds) return e;
+  hipLaunchKernelGGL(k_mark_selected, dim3(nblk(n_rounds * (size_t)t, 256)), dim3(256), 0, st, sel, rok, t, n_rounds, need);
+  return hipGetLastError();
+}
+
 hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, int entries, uint32_t* tbl, uint32_t* zs,
                                 hipStream_t st) {
   if (!n) return hipSuccess;

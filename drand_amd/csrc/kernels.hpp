@@ -115,6 +115,10 @@ hipError_t launch_leaf_check(int sig_g2, const uint32_t* entries, size_t m, cons
 hipError_t launch_group_check_vm(int sig_g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_aff,
                                  const uint32_t* key_h,
                                  uint32_t* pairs, uint8_t* live, uint8_t* pass, hipStream_t st);
+// G2-signature group checks with the cofactor clearing inside the pairing program (k_vm.hip k_vm_pairing_c)
+size_t group_check_c_pair_words();
+hipError_t launch_group_check_vm_c(const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_aff, uint32_t* pairs,
+                                   uint8_t* live, uint8_t* done, uint8_t* pass, hipStream_t st);
 hipError_t launch_leaf_check_vm(int sig_g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
                                 const uint32_t* key_aff, const uint32_t* key_h, const uint8_t* status, uint32_t* pairs,
                                 uint8_t* live, uint8_t* done, uint8_t* verdict, hipStream_t st);
@@ -154,6 +158,8 @@ hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const 
 // tbl (G2): per valid partial (ok) the odd multiples P, 3P, ..., (2 entries - 1) P affine 28-bit (entries = 4 or 8,
 // 64 words each) from the partials' affine points (12 x 32-bit AOS); zs: wnaf_table_scratch_bytes(n, entries) of
 // scratch (the batched inversion's Z's); unused for G1
+hipError_t launch_mark_selected(const uint32_t* sel, const uint8_t* rok, int t, size_t n_rounds, size_t np, uint8_t* need,
+                                hipStream_t st);
 hipError_t launch_wnaf_table_g2(const uint32_t* paff, const uint8_t* ok, size_t n, int entries, uint32_t* tbl, uint32_t* zs,
                                 hipStream_t st);
 size_t wnaf_table_scratch_bytes(size_t n, int entries);

@@ -408,13 +408,24 @@ def miller_loop(Ps, Qs):
     return f.conj()
 
 
+# The state of a cyclotomic squaring run is materialised (LIN ops) every CYC_MAT squarings and before each
+# multiplication: in between, the next squaring's product operands take the unmaterialised linear combinations
+# (up to MAXT terms; L._norm adds a LIN op where one would exceed it). Every squaring materialised: 746 phases for
+# the final exponentiation; every third: 546 (the 2-pair check 1162 -> 950 with the critical-path schedule).
+CYC_MAT = 3
+
+
 def cyc_exp_u(a):
     acc = a
+    it = 0
     for b in range(62, -1, -1):
-        acc = acc.cyc_sqr().mat()
+        acc = acc.cyc_sqr()
+        it += 1
+        if it % CYC_MAT == 0 or (U_ABS >> b) & 1:
+            acc = acc.mat()
         if (U_ABS >> b) & 1:
             acc = (acc * a).mat()
-    return acc.conj()
+    return acc.mat().conj()
 
 
 def final_exp(f):
@@ -437,6 +448,80 @@ FROB6_C2 = [gc.f2pow(XI, 2 * (P ** k - 1) // 3) for k in (1, 2, 3)]
 FROB12_C = [gc.f2pow(XI, (P ** k - 1) // 6) for k in (1, 2, 3)]
 
 
+# ----------------------------------------------------------------------------------------- G2 cofactor clearing
+# [h_eff] Q by the endomorphism method of RFC 9380 Appendix G.3, the same steps as fp2_28.hpp g2_clear28 (the group
+# check of G2-signature schemes clears the RLC sum of the uncleared hash points): in the program its ~128 doublings
+# run as ~3 product phases each on the lanes instead of on one lane (k_vm_prep_groups<fp2>, 3.9 ms per check).
+# Jacobian formulas without exceptional-case tests: an exceptional case leaves Z = 0, which every later step keeps,
+# so the program also outputs Z and a zero Z sends the check to the exact one-lane path (k_vm.hip k_vm_pairing_c).
+PSI_X = gc.f2inv(gc.f2pow(XI, (P - 1) // 3))
+PSI_Y = gc.f2inv(gc.f2pow(XI, (P - 1) // 2))
+PSI2_X = gc.f2mul(gc.f2pow(PSI_X, P), PSI_X)
+PSI2_Y = gc.f2mul(gc.f2pow(PSI_Y, P), PSI_Y)
+assert PSI2_X[1] == 0 and PSI2_Y[1] == 0
+
+
+def g2_dbl(T):
+    """dbl-2009-l (a = 0)"""
+    X, Y, Z = T
+    A, B = X.sqr(), Y.sqr()
+    C = B.sqr()
+    D = ((X + B).sqr() - A - C).dbl()
+    E = A.dbl() + A
+    X3 = E.sqr() - D.dbl()
+    Y3 = E * (D - X3) - C.dbl().dbl().dbl()
+    Z3 = (Y * Z).dbl()
+    return (X3, Y3, Z3)
+
+
+def g2_add(T1, T2):
+    """add-2007-bl, both Jacobian"""
+    X1, Y1, Z1 = T1
+    X2, Y2, Z2 = T2
+    z1z1, z2z2 = Z1.sqr(), Z2.sqr()
+    u1, u2 = X1 * z2z2, X2 * z1z1
+    s1, s2 = Y1 * (Z2 * z2z2), Y2 * (Z1 * z1z1)
+    h = u2 - u1
+    i = h.dbl().sqr()
+    j = h * i
+    r = (s2 - s1).dbl()
+    v = u1 * i
+    X3 = r.sqr() - j - v.dbl()
+    Y3 = r * (v - X3) - (s1 * j).dbl()
+    Z3 = ((Z1 + Z2).sqr() - z1z1 - z2z2) * h
+    return (X3, Y3, Z3)
+
+
+def g2_neg(T):
+    return (T[0], -T[1], T[2])
+
+
+def g2_psi(T):
+    return (T[0].conj() * F2.const(PSI_X), T[1].conj() * F2.const(PSI_Y), T[2].conj())
+
+
+def g2_psi2(T):
+    return (T[0].mul_fp(L.const(PSI2_X[0])), T[1].mul_fp(L.const(PSI2_Y[0])), T[2])
+
+
+def g2_mul_uabs(T):
+    """[|u|] T: the doubling runs between |u|'s set bits (fp2_28.hpp uabs_run)"""
+    acc = T
+    for r, k in enumerate((1, 2, 3, 9, 32, 16)):
+        for _ in range(k):
+            acc = g2_dbl(acc)
+        if r < 5:
+            acc = g2_add(acc, T)
+    return acc
+
+
+def g2_clear(p):
+    t1 = g2_neg(g2_mul_uabs(p))
+    t3 = g2_add(g2_psi2(g2_dbl(p)), g2_neg(g2_psi(p)))
+    t2 = g2_neg(g2_mul_uabs(g2_add(t1, g2_psi(p))))
+    return g2_add(g2_add(g2_add(t3, t2), g2_neg(t1)), g2_neg(p))
+
+
 def _fp12_input(prefix):
     c = [L.node(PROG.inp("%s%d" % (prefix, i))) for i in range(12)]
     return F12(F6(F2(c[0], c[1]), F2(c[2], c[3]), F2(c[4], c[5])), F6(F2(c[6], c[7]), F2(c[8], c[9]), F2(c[10], c[11])))
@@ -446,6 +531,8 @@ def build_tag(tag):
     """Programs: NP1 / NP2 = the full check of 1 / 2 pairs; ML1 = the Miller loop of one pair (f out, for
     multi-pairings of many pairs run one workgroup per pair); MUL12 = f * g; FE = final exponentiation."""
     global PROG
+    if tag == "NP2C":
+        return build_np2c()
     if tag.startswith("NP"):
         return build(int(tag[2:]))
     PROG = Prog()
@@ -493,6 +580,33 @@ def build(np_):
     return prog, outs
 
 
+def build_np2c():
+    """The group check of a G2-signature scheme, e(P0, [h_eff] B) e(P1, Q1) == 1, with the RLC hash sum B entering
+    uncleared and Jacobian (B.x0 .. B.z1): cofactor clearing, affine form (one inversion), 2-pair Miller loop, final
+    exponentiation. Outputs: the 12 coordinates of the result, then Z of [h_eff] B (c0, c1)."""
+    global PROG
+    PROG = Prog()
+    p0 = (L.node(PROG.inp("P0.x")), L.node(PROG.inp("P0.y")))
+    b = tuple(F2(L.node(PROG.inp("B.%s0" % c)), L.node(PROG.inp("B.%s1" % c))) for c in "xyz")
+    p1 = (L.node(PROG.inp("P1.x")), L.node(PROG.inp("P1.y")))
+    q1 = (F2(L.node(PROG.inp("Q1.x0")), L.node(PROG.inp("Q1.x1"))), F2(L.node(PROG.inp("Q1.y0")), L.node(PROG.inp("Q1.y1"))))
+    X, Y, Z = g2_clear(b)
+    Z = Z.mat()
+    zi = Z.inv()
+    zi2 = zi.sqr()
+    q0 = ((X * zi2).mat(), (Y * (zi2 * zi)).mat())
+    r = final_exp(miller_loop([p0, p1], [q0, q1]))
+    outs = []
+    for c in r.coords() + [Z.a, Z.b]:
+        m = c.mat()
+        if not m.t:
+            raise RuntimeError("zero output coordinate")
+        outs.append(m.single())
+    prog = PROG
+    PROG = None
+    return prog, outs
+
+
 # ----------------------------------------------------------------------------------------- scheduling
 def deps(n):
     k = n["kind"]
@@ -505,7 +619,11 @@ def deps(n):
 
 
 def schedule(prog, outs):
-    """Greedy ASAP list scheduling into phases: MUL phase (<= LANES products), then LIN sub-phases, then INV."""
+    """Critical-path list scheduling into phases of one kind (MUL: <= LANES products, LIN: <= LANES, INV: one op).
+    Each step runs the kind whose ready set holds the op with the longest path to an output (its height), filled by
+    height. The r02-r04 ASAP order ran every ready LIN op right after each product phase, so a chain that needed only
+    products (the G2 cofactor clearing of NP2C beside the other pair's Miller loop) paid a LIN phase after each of its
+    product phases: NP2C 1790 -> 1572 phases, ML1 410 -> 337, NP2 1162 -> 1150 (before CYC_MAT)."""
     nodes = prog.nodes
     # dead-code elimination from the outputs
     live = set(outs)
@@ -516,8 +634,11 @@ def schedule(prog, outs):
     pending = [i for i, n in enumerate(nodes) if n["kind"] not in ("in", "const") and i in live]
     users = {}
     for i in pending:
-        for d in deps(nodes[i]):
+        for d in set(deps(nodes[i])):
             users.setdefault(d, []).append(i)
+    height = {}
+    for i in sorted(pending, reverse=True):  # users come after their operands in node order
+        height[i] = 1 + max((height[u] for u in users.get(i, [])), default=0)
     ndeps = {i: len(set(d for d in deps(nodes[i]) if d not in done)) for i in pending}
     ready = {"mul": [], "lin": [], "inv": []}
     for i in pending:
@@ -525,31 +646,28 @@ def schedule(prog, outs):
             ready[nodes[i]["kind"]].append(i)
     phases = []
     remaining = len(pending)
-
-    def finish(batch):
-        nonlocal remaining
+    while remaining:
+        best = None
+        for kind in ("mul", "lin", "inv"):
+            if ready[kind]:
+                m = max(height[i] for i in ready[kind])
+                if best is None or m > best[0]:
+                    best = (m, kind)
+        if best is None:
+            raise RuntimeError("scheduling deadlock")
+        kind = best[1]
+        ready[kind].sort(key=lambda i: (-height[i], i))
+        cap = 1 if kind == "inv" else LANES
+        batch, ready[kind] = ready[kind][:cap], ready[kind][cap:]
+        phases.append((kind, batch))
         for i in batch:
             done.add(i)
             remaining -= 1
         for i in batch:
             for u in set(users.get(i, [])):
-                ndeps[u] -= len([d for d in set(deps(nodes[u])) if d == i])
+                ndeps[u] -= 1
                 if ndeps[u] == 0:
                     ready[nodes[u]["kind"]].append(u)
-
-    while remaining:
-        progressed = False
-        for kind, cap in (("mul", LANES), ("lin", LANES), ("inv", 1)):
-            while ready[kind]:
-                ready[kind].sort()
-                batch, ready[kind] = ready[kind][:cap], ready[kind][cap:]
-                phases.append((kind, batch))
-                finish(batch)
-                progressed = True
-                if kind == "mul":
-                    break  # re-offer LIN / INV work between product phases
-        if not progressed:
-            raise RuntimeError("scheduling deadlock")
     return phases, live
 
 
@@ -661,7 +779,38 @@ def validate_split(progs):
     assert fe(mul(mul(ml(Pa, G2), ml(negG1, Qa)), mul(ml(G1, G2), ml(negG1, G2)))) == one
 
 
+def validate_np2c(prog, outs, phases, slot, nslots):
+    """e(pk, [h_eff] B) e(-G1, [sk][h_eff] B) = 1 for an uncleared B given in Jacobian form with a random Z, != 1
+    for a wrong signature sum; the Z output is that of [h_eff] B (nonzero)."""
+    B = _bls_points()
+    rng = random.Random(3)
+    h = B.iso_map_g2(B.sswu_g2((rng.randrange(P), rng.randrange(P))))
+    assert B.g2_on_curve(h)
+    hh = B.ec_mul(B.FP2, h, B.H_EFF_G2)
+    sk = rng.randrange(2, B.R)
+    pk = B.ec_mul(B.FP, B.G1_GEN, sk)
+    sig = B.ec_mul(B.FP2, hh, sk)
+    ng1 = B.ec_neg(B.FP, B.G1_GEN)
+    z = (rng.randrange(1, P), rng.randrange(P))
+    z2 = B.f2mul(z, z)
+    jx, jy = B.f2mul(h[0], z2), B.f2mul(h[1], B.f2mul(z2, z))
+
+    def run(q1):
+        inp = {"P0.x": pk[0], "P0.y": pk[1], "B.x0": jx[0], "B.x1": jx[1], "B.y0": jy[0], "B.y1": jy[1],
+               "B.z0": z[0], "B.z1": z[1], "P1.x": ng1[0], "P1.y": ng1[1],
+               "Q1.x0": q1[0][0], "Q1.x1": q1[0][1], "Q1.y0": q1[1][0], "Q1.y1": q1[1][1]}
+        return evaluate(prog, outs, phases, slot, nslots, inp)
+
+    one = [1] + [0] * 11
+    res = run(sig)
+    assert res[:12] == one, "NP2C: e(pk, [h]B) e(-G1, sk [h]B) != 1"
+    assert res[12:] != [0, 0]
+    assert run(B.ec_add(B.FP2, sig, B.G2_GEN))[:12] != one, "NP2C accepted a wrong signature sum"
+
+
 def validate(np_, prog, outs, phases, slot, nslots):
+    if np_ == "NP2C":
+        return validate_np2c(prog, outs, phases, slot, nslots)
     if isinstance(np_, str):
         if not np_.startswith("NP"):
             return  # checked in validate_split
@@ -751,7 +900,8 @@ def emit(progs):
         lines.append("constexpr int %s_NPHASES = %d, %s_NSLOTS = %d, %s_NCONST = %d;" % (
             tag, len(phases), tag, nslots, tag, len(consts)))
         lines.append("__device__ __constant__ uint32_t %s_INPUT_SLOT[%d] = {%s};" % (tag, len(ins), ", ".join(map(str, ins))))
-        lines.append("__device__ __constant__ uint32_t %s_OUTPUT_SLOT[12] = {%s};" % (tag, ", ".join(str(slot[o]) for o in outs)))
+        lines.append("__device__ __constant__ uint32_t %s_OUTPUT_SLOT[%d] = {%s};" % (
+            tag, len(outs), ", ".join(str(slot[o]) for o in outs)))
         lines.append("__device__ __constant__ uint32_t %s_CONST_SLOT[%d] = {%s};" % (
             tag, len(consts), ", ".join(str(s) for s, _ in consts)))
         lines.append("__device__ __constant__ uint32_t %s_CONST_VAL[%d][14] = {%s};" % (
@@ -764,7 +914,7 @@ def emit(progs):
     return "\n".join(lines)
 
 
-TAGS = ("NP1", "NP2", "ML1", "MUL12", "FE")
+TAGS = ("NP1", "NP2", "ML1", "MUL12", "FE", "NP2C")
 
 
 def build_all():
