@@ -416,12 +416,26 @@ dh::msm_geom geom_for(size_t gsize, int parts = 1) {
   g.nbuck = (1u << (c - 1)) + 1;  // signed digits: |d| in [1, 2^(c-1)] (k_msm.hip: signed_digit)
   // bucket reduction: segments of ~8 digits, one thread each (k_msm_segsum): 16 additions + the segment's offset
   // multiple per thread, then a log-depth tree
-  uint32_t nseg = std::max(1u, std::min(8192u, g.nbuck / 8));
+  uint32_t nseg = std::max(1u, std::min(8192u, g.nbuck / 8));  // a power of two (nbuck = 2^(c-1) + 1)
   g.nseg = nseg;
   g.seglen = (g.nbuck - 1 + nseg - 1) / nseg;
   g.halves = (uint32_t)parts;
   g.half_stride = 0;  // set by the caller: the point-array offset of the endomorphism images
   return g;
+}
+
+// Bucket-reduction segments for a level of ngroups groups (nsets point sets): as many segments per (set, group, window)
+// row as keep ~256k segment threads busy, at most nbuck / 8. Each extra segment costs its offset multiple (segoff:
+// ~log2 k doublings) and a tree level; with thousands of groups (the bisection's 256- and 32-round levels) the rows
+// alone fill the chip, and geom_for's fixed 8-bucket segments had doubled the reduction's additions there (a
+// 129-bucket row: 16 segments = 256 + ~150 segoff additions against 256 + 7 for 2).
+static void fit_segments(dh::msm_geom& g, size_t ngroups, size_t nsets) {
+  const size_t rows = std::max<size_t>(1, nsets * ngroups * (size_t)g.nwin);
+  const size_t want = ((size_t)1 << 18) / rows + 1;
+  size_t nseg = std::max<size_t>(1, std::min<size_t>({want, (size_t)g.nseg}));
+  if (nseg > 64) nseg &= ~(size_t)63;  // whole waves per row beyond 64 segments (k_msm.hip k_msm_segred28)
+  g.nseg = (uint32_t)nseg;
+  g.seglen = (g.nbuck - 1 + g.nseg - 1) / g.nseg;
 }
 
 constexpr size_t JAC_WORDS_G1 = 36, JAC_WORDS_G2 = 72;
@@ -855,6 +869,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
     dh::msm_geom g = geom_for(gsize, parts);
     g.half_stride = (uint32_t)n;
     const size_t ngroups = (m + gsize - 1) / gsize;
+    fit_segments(g, ngroups, 2);
     const bool pre = level == 0 && presorted;
     dh::msm_ws ws{};
     if (pre) {

@@ -114,6 +114,27 @@ DH_DEV void fr_to_words(const fr& a, uint32_t out[8]) {
   for (int i = 0; i < 8; i++) out[i] = c.v[i];
 }
 
+// the shorter of w and r - w (little-endian words) into k; true when it is r - w, whose digits the caller negates
+// ([-(r - w)] P = [w] P on the order-r subgroup). A Lagrange coefficient of the first t signers is +-C(t, k) mod r: half
+// of them sit just below r, and their recoding as r - w is a ~31-bit number instead of a 255-bit one.
+DH_DEV bool fr_short(const uint32_t w[8], uint32_t k[8]) {
+  uint32_t n[8];
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) n[i] = __builtin_subc(FR_MOD[i], w[i], br, &br);
+  bool less = false, eq = true;  // n < w, from the top word
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {
+    if (eq && n[i] != w[i]) {
+      less = n[i] < w[i];
+      eq = false;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = less ? n[i] : w[i];
+  return less;
+}
+
 // non-adjacent form of k < 2^255 (little-endian words) as positive / negative digit masks over 256 positions
 // width-4 NAF of a scalar w < 2^255 (little-endian words): digit b in nibble b (word b / 8, bits 4 (b % 8)), 0 = zero,
 // v in 1..4 = +(2v - 1), v in 9..12 = -(2(v - 8) - 1): odd digits in [-7, 7], each followed by at least three zeros

@@ -85,6 +85,61 @@ __global__ void k_msm_scatter(const uint32_t* __restrict__ pidx, const uint32_t*
   }
 }
 
+// The counting sort through LDS. A workgroup takes a tile of consecutive entries and one slab of the key space (at
+// most SLAB_MAX consecutive keys: one window's 32,769 buckets at c = 16, or the windows of the tile's groups at the
+// bisection's small c), and counts its entries' digits that fall in the slab into an LDS histogram (ds_add: no
+// global traffic per entry). The histogram pass flushes the nonzero LDS counts into the global counts; the scatter
+// pass claims each nonzero (tile, key)'s range of the sorted list with ONE global atomic and then places the tile's
+// entries by LDS atomics on the claimed bases. Tiles hold enough entries that the digits outnumber the slab's keys
+// several times over (sort_plan), so the global atomics fall from one per digit to about one per key and tile.
+constexpr uint32_t SORT_T = 1024, SLAB_MAX = 36864;  // 144 KiB of counters: one workgroup per CU
+
+template <bool SCATTER>
+__global__ __launch_bounds__(SORT_T) void k_msm_sort_lds(const uint32_t* __restrict__ pidx, const uint32_t* __restrict__ sidx,
+                                                         const uint32_t* __restrict__ grp, size_t m, const uint4* __restrict__ scal,
+                                                         msm_geom g, size_t nk, uint32_t tile, uint32_t slab,
+                                                         uint32_t* __restrict__ gcnt, uint32_t* __restrict__ list) {
+  extern __shared__ uint32_t h[];  // slab counters (dynamic: slab x 4 bytes)
+  const size_t e0 = (size_t)blockIdx.x * tile, e1 = min(m, e0 + tile);
+  const size_t rowkeys = (size_t)g.nwin * g.nbuck;
+  // the tile's key span: its groups' rows (entries of a group are consecutive without grp), else every key
+  const size_t kb = grp ? 0 : (e0 / g.gsize) * rowkeys, ke = grp ? nk : min(nk, ((e1 - 1) / g.gsize + 1) * rowkeys);
+  const size_t K0 = kb + (size_t)blockIdx.y * slab;
+  if (K0 >= ke) return;  // workgroup-uniform, before any barrier
+  const uint32_t ns = (uint32_t)min((size_t)slab, ke - K0);
+  for (uint32_t k = threadIdx.x; k < ns; k += SORT_T) h[k] = 0;
+  __syncthreads();
+  // f(key in the slab, point index | sign) for every digit of the tile's entries
+  auto each = [&](auto&& f) {
+    for (size_t e = e0 + threadIdx.x; e < e1; e += SORT_T) {
+      const uint32_t idx0 = pidx[e];
+      const uint4 s = scal[sidx ? sidx[e] : idx0];
+      const size_t gi = entry_group(grp, e, g.gsize);
+      for (uint32_t hh = 0; hh < g.halves; hh++) {
+        const uint4 sh = half_scalar(s, hh, g);
+        const uint32_t idx = idx0 + hh * g.half_stride;
+        uint32_t carry = 0;
+        for (int w = 0; w < g.nwin; w++) {
+          const int32_t d = signed_digit(sh, w, g, carry);
+          const size_t key = (gi * g.nwin + w) * g.nbuck + (uint32_t)(d < 0 ? -d : d);
+          if (d && key - K0 < ns) f((uint32_t)(key - K0), d < 0 ? (idx | NEG_BIT) : idx);
+        }
+      }
+    }
+  };
+  each([&](uint32_t k, uint32_t) { atomicAdd(&h[k], 1u); });
+  __syncthreads();
+  if constexpr (!SCATTER) {
+    for (uint32_t k = threadIdx.x; k < ns; k += SORT_T)
+      if (h[k]) atomicAdd(&gcnt[K0 + k], h[k]);
+  } else {
+    for (uint32_t k = threadIdx.x; k < ns; k += SORT_T)
+      if (h[k]) h[k] = atomicAdd(&gcnt[K0 + k], h[k]);  // this tile's base in the key's range of the list
+    __syncthreads();
+    each([&](uint32_t k, uint32_t v) { list[atomicAdd(&h[k], 1u)] = v; });
+  }
+}
+
 // exclusive scan, 3 phases: per-block totals, scan of totals (one block), final per-block scan
 constexpr int SCAN_T = 256, SCAN_I = 16, SCAN_B = SCAN_T * SCAN_I;
 
@@ -243,10 +298,51 @@ hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32
   ws.max_entries = msm_entries(g, m);
   hipError_t e = hipMemsetAsync(ws.cnt, 0, nk * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
-  if (m) hipLaunchKernelGGL(k_msm_hist, dim3(nblk(m, 256)), dim3(256), 0, st, pidx, sidx, grp, m, scal, g, ws.cnt);
+  // DRANDHIP_SORT_GLOBAL=1 (experiments): the one-global-atomic-per-digit sort
+  static const bool global_sort = [] {
+    const char* v = getenv("DRANDHIP_SORT_GLOBAL");
+    return v && atoi(v) == 1;
+  }();
+  // the LDS sort's plan: tiles of about density x the slab's keys in digits (DRANDHIP_SORT_DENSITY), slabs of at
+  // most SLAB_MAX keys over the keys a tile can touch
+  dim3 grid;
+  uint32_t tile = 0, slab = 0;
+  if (m && !global_sort) {
+    static const size_t density = [] {
+      const char* v = getenv("DRANDHIP_SORT_DENSITY");
+      const long d = v ? atol(v) : 0;
+      return (size_t)(d >= 1 && d <= 256 ? d : 8);
+    }();
+    const size_t digits = (size_t)g.halves * g.nwin, rowkeys = (size_t)g.nwin * g.nbuck;
+    // DRANDHIP_SORT_SLAB: the LDS slab in keys (smaller slabs let the workgroups share a CU with the kernels beside them)
+    static const size_t slab_max = [] {
+      const char* v = getenv("DRANDHIP_SORT_SLAB");
+      const long d = v ? atol(v) : 0;
+      return (size_t)(d >= 1024 && d <= SLAB_MAX ? d : SLAB_MAX);
+    }();
+    static const hipError_t lds_attr = [] {  // dynamic LDS beyond 64 KiB
+      hipError_t a = hipFuncSetAttribute((const void*)k_msm_sort_lds<false>, hipFuncAttributeMaxDynamicSharedMemorySize, SLAB_MAX * 4);
+      hipError_t b = hipFuncSetAttribute((const void*)k_msm_sort_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, SLAB_MAX * 4);
+      return a != hipSuccess ? a : b;
+    }();
+    if (lds_attr != hipSuccess) return lds_attr;
+    const size_t t = std::min(m, std::max<size_t>(SORT_T, density * std::min<size_t>(nk, slab_max) / digits));
+    // keys one tile can touch: every key with grp, else the rows of at most t / gsize + 2 consecutive groups
+    const size_t span = grp ? nk : std::min(nk, std::min<size_t>(ngroups, (t - 1) / g.gsize + 2) * rowkeys);
+    const size_t nslab = (span + slab_max - 1) / slab_max;
+    tile = (uint32_t)t;
+    slab = (uint32_t)((span + nslab - 1) / nslab);
+    grid = dim3((unsigned)((m + t - 1) / t), (unsigned)nslab);
+  }
+  if (m && global_sort) hipLaunchKernelGGL(k_msm_hist, dim3(nblk(m, 256)), dim3(256), 0, st, pidx, sidx, grp, m, scal, g, ws.cnt);
+  if (m && !global_sort)
+    hipLaunchKernelGGL(k_msm_sort_lds<false>, grid, dim3(SORT_T), slab * 4, st, pidx, sidx, grp, m, scal, g, nk, tile, slab, ws.cnt, ws.list);
   if ((e = launch_scan(ws.cnt, nk, ws.off, ws.scan_tmp, st)) != hipSuccess) return e;
   if ((e = hipMemcpyAsync(ws.cnt, ws.off, nk * sizeof(uint32_t), hipMemcpyDeviceToDevice, st)) != hipSuccess) return e;
-  if (m) hipLaunchKernelGGL(k_msm_scatter, dim3(nblk(m, 256)), dim3(256), 0, st, pidx, sidx, grp, m, scal, g, ws.cnt, ws.list);
+  if (m && global_sort)
+    hipLaunchKernelGGL(k_msm_scatter, dim3(nblk(m, 256)), dim3(256), 0, st, pidx, sidx, grp, m, scal, g, ws.cnt, ws.list);
+  if (m && !global_sort)
+    hipLaunchKernelGGL(k_msm_sort_lds<true>, grid, dim3(SORT_T), slab * 4, st, pidx, sidx, grp, m, scal, g, nk, tile, slab, ws.cnt, ws.list);
   return hipGetLastError();
 }
 
@@ -623,6 +719,76 @@ DH_DEV void seg_run(const uint32_t* __restrict__ buckets, const uint32_t* __rest
     tot = C::template addx<EXACT>(tot, run);
   }
 }
+// points through LDS for the wave-level trees: word-major (word k of thread i at buf[k * nthr + i]: one ds_read_b32
+// per word across the wave, conflict-free); infinity travels as Z = 0, like stj28
+DH_DEV void lds_put(uint32_t* buf, int nthr, int i, int k0, const f28& a) {
+#pragma unroll
+  for (int k = 0; k < 14; k++) buf[(k0 + k) * nthr + i] = a.l[k];
+}
+DH_DEV void lds_get(const uint32_t* buf, int nthr, int i, int k0, f28& a) {
+#pragma unroll
+  for (int k = 0; k < 14; k++) a.l[k] = buf[(k0 + k) * nthr + i];
+}
+DH_DEV void lds_put(uint32_t* buf, int nthr, int i, int k0, const f228& a) {
+  lds_put(buf, nthr, i, k0, a.c0);
+  lds_put(buf, nthr, i, k0 + 14, a.c1);
+}
+DH_DEV void lds_get(const uint32_t* buf, int nthr, int i, int k0, f228& a) {
+  lds_get(buf, nthr, i, k0, a.c0);
+  lds_get(buf, nthr, i, k0 + 14, a.c1);
+}
+template <class C>
+constexpr int lds_words() { return 3 * 14 * (C::EW / W28); }
+template <class C>
+DH_DEV void lds_put_pt(uint32_t* buf, int nthr, int i, const typename C::P& a) {
+  constexpr int EL = 14 * (C::EW / W28);
+  lds_put(buf, nthr, i, 0, a.x);
+  lds_put(buf, nthr, i, EL, a.y);
+  typename C::E z = a.z;
+  if (a.inf) set_zero(z);
+  lds_put(buf, nthr, i, 2 * EL, z);
+}
+template <class C>
+DH_DEV typename C::P lds_get_pt(const uint32_t* buf, int nthr, int i) {
+  constexpr int EL = 14 * (C::EW / W28);
+  typename C::P r;
+  lds_get(buf, nthr, i, 0, r.x);
+  lds_get(buf, nthr, i, EL, r.y);
+  lds_get(buf, nthr, i, 2 * EL, r.z);
+  r.inf = z_all_zero(r.z);
+  return r;
+}
+// a + the point in LDS slot i, its coordinates read where the formula uses them (G2: fewer values live)
+template <class C, bool EXACT>
+DH_DEV typename C::P add_lds(const typename C::P& a, const uint32_t* buf, int nthr, int i) {
+  if constexpr (C::PARTS == 4) {
+    constexpr int EL = 28;
+    f228 z;
+    lds_get(buf, nthr, i, 2 * EL, z);
+    return j228_add_ld<EXACT>(a, z_all_zero(z), [&](int k) { f228 c; lds_get(buf, nthr, i, k * EL, c); return c; });
+  } else {
+    return C::template addx<EXACT>(a, lds_get_pt<C>(buf, nthr, i));
+  }
+}
+// the tree over aligned runs of `span` lanes (a power of two <= 64) of each wave: lane l, l % span == 0, ends with the
+// sum of lanes [l, l + span). Every thread of the workgroup calls it (barriers); buf: lds_words<C>() x blockDim words.
+// The inputs are exact (stored points), so a poisoned sum is recomputed with the exact formulas on the spot.
+template <class C>
+DH_DEV typename C::P wave_tree(typename C::P acc, uint32_t* buf, uint32_t span) {
+  const int nthr = blockDim.x, i = threadIdx.x, lane = i & 63;
+#pragma unroll 1
+  for (uint32_t step = 1; step < span; step <<= 1) {
+    lds_put_pt<C>(buf, nthr, i, acc);
+    __syncthreads();
+    if ((lane & (2 * step - 1)) == 0) {
+      typename C::P s = add_lds<C, false>(acc, buf, nthr, i + (int)step);
+      acc = C::poisoned(s) ? add_lds<C, true>(acc, buf, nthr, i + (int)step) : s;
+    }
+    __syncthreads();
+  }
+  return acc;
+}
+
 template <class C>
 __global__ __launch_bounds__(256, C::OCC) void k_msm_segsum28(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ off,
                                                               msm_geom g, size_t ngw, size_t rows_per_set, uint32_t* __restrict__ segs,
@@ -666,41 +832,55 @@ __global__ __launch_bounds__(256, C::OCC) void k_msm_segoff28(msm_geom g, size_t
   stj28<C>(segs, t, r);
 }
 
+// The segment values of a (set, group, window) row summed by wave-level trees through LDS (r04: a tree of log2(nseg)
+// launches of one addition per thread, 12 at level 0). k_msm_rowtree28: a row's nseg values sit on lpr lanes (nseg
+// rounded up to a power of two, the extra lanes holding the identity) when nseg <= 64, and wave_tree leaves the row sum
+// in its first lane; a longer row (a multiple of 64 segments: geom_for, fit_segments) covers whole waves, each leaving
+// one partial, and k_msm_rowred28 (one wave per row) sums the row's nseg / 64 partials the same way.
 template <class C>
-__global__ __launch_bounds__(256, C::OCC) void k_msm_tree28(uint32_t* __restrict__ v, size_t rows, uint32_t stride, uint32_t width,
-                                                            uint32_t half) {
+__global__ __launch_bounds__(256, C::OCC) void k_msm_rowtree28(const uint32_t* __restrict__ segs, uint32_t nseg, size_t ngw,
+                                                               uint32_t lpr, uint32_t span, uint32_t* __restrict__ out) {
+  __shared__ uint32_t buf[lds_words<C>() * 256];
   const size_t t = gtid();
-  if (t >= rows * half) return;
-  const size_t r = t / half, c = t % half;
-  if (c + half >= width) return;
-  const size_t i = r * stride + c;
-  const typename C::P a = ldj28<C>(v, i);
-  const uint32_t* b = v + (size_t)3 * C::EW * (i + half);
-  typename C::P s = C::template add_mem<false>(a, b);
-  if (C::poisoned(s)) s = C::template add_mem<true>(a, b);
-  stj28<C>(v, i, s);
+  typename C::P acc = C::inf();
+  if (t < ngw * lpr && t % lpr < nseg) acc = ldj28<C>(segs, (t / lpr) * nseg + t % lpr);
+  acc = wave_tree<C>(acc, buf, span);
+  if (t < ngw * lpr && (t & (span - 1)) == 0) stj28<C>(out, t / span, acc);
+}
+template <class C>
+__global__ __launch_bounds__(64) void k_msm_rowred28(const uint32_t* __restrict__ parts_in, uint32_t parts, uint32_t* __restrict__ rowsum) {
+  __shared__ uint32_t buf[lds_words<C>() * 64];
+  const size_t row = blockIdx.x;
+  typename C::P acc = C::inf();
+  for (uint32_t k = threadIdx.x; k < parts; k += 64) {
+    const uint32_t* p = parts_in + (size_t)3 * C::EW * (row * parts + k);
+    const typename C::P s = C::template add_mem<false>(acc, p);
+    acc = C::poisoned(s) ? C::template add_mem<true>(acc, p) : s;
+  }
+  acc = wave_tree<C>(acc, buf, 64);
+  if (threadIdx.x == 0) stj28<C>(rowsum, row, acc);
 }
 
 template <class C, bool EXACT>
-DH_DEV typename C::P horner28(const uint32_t* __restrict__ segs, const msm_geom& g, size_t t) {
-  typename C::P acc = ldj28<C>(segs, (t * g.nwin + g.nwin - 1) * g.nseg);
+DH_DEV typename C::P horner28(const uint32_t* __restrict__ rowsum, const msm_geom& g, size_t t) {
+  typename C::P acc = ldj28<C>(rowsum, t * g.nwin + g.nwin - 1);
 #pragma unroll 1
   for (int w = g.nwin - 2; w >= 0; w--) {
 #pragma unroll 1
     for (int k = 0; k < g.c; k++) acc = C::dbl(acc);
-    acc = C::template add_mem<EXACT>(acc, segs + (size_t)3 * C::EW * ((t * g.nwin + w) * g.nseg));
+    acc = C::template add_mem<EXACT>(acc, rowsum + (size_t)3 * C::EW * (t * g.nwin + w));
   }
   return acc;
 }
 
-// per (set, group): Horner over the windows, out = 12 x 32-bit Montgomery Jacobian (jac_inf for the identity)
+// per (set, group): Horner over the windows' row sums, out = 12 x 32-bit Montgomery Jacobian (jac_inf for the identity)
 template <class C>
-__global__ __launch_bounds__(64) void k_msm_windows28(const uint32_t* __restrict__ segs, msm_geom g, size_t ngroups,
+__global__ __launch_bounds__(64) void k_msm_windows28(const uint32_t* __restrict__ rowsum, msm_geom g, size_t ngroups,
                                                       uint32_t* __restrict__ out) {
   const size_t t = gtid();
   if (t >= ngroups) return;
-  typename C::P acc = horner28<C, false>(segs, g, t);
-  if (C::poisoned(acc)) acc = horner28<C, true>(segs, g, t);
+  typename C::P acc = horner28<C, false>(rowsum, g, t);
+  if (C::poisoned(acc)) acc = horner28<C, true>(rowsum, g, t);
   jac<typename C::F> r = jac_inf<typename C::F>();
   if (!acc.inf) {
     r.x = C::out(acc.x);
@@ -745,16 +925,28 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     }
   }
   const size_t rows = ngroups * g.nwin, ngw = (size_t)nsets * rows;
+  if (g.nseg > 64 && g.nseg % 64) return hipErrorInvalidValue;  // whole waves per row (geom_for, fit_segments)
   hipLaunchKernelGGL(k_msm_segsum28<C>, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs,
                      ws.runs);
   if (g.nseg > 1)
     hipLaunchKernelGGL(k_msm_segoff28<C>, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, g, ngw, ws.segs, ws.runs);
-  for (uint32_t width = g.nseg; width > 1;) {
-    const uint32_t half = (width + 1) / 2;
-    hipLaunchKernelGGL(k_msm_tree28<C>, dim3(nblk(ngw * half, 256)), dim3(256), 0, st, ws.segs, ngw, g.nseg, width, half);
-    width = half;
+  // row sums: ws.runs (free after the offsets) for nseg <= 64; else the waves' partials go to ws.runs and the row sums
+  // to ws.segs
+  uint32_t lpr = g.nseg, span = 64;
+  if (g.nseg <= 64) {
+    for (lpr = 1; lpr < g.nseg;) lpr *= 2;
+    span = lpr;
   }
-  hipLaunchKernelGGL(k_msm_windows28<C>, dim3(nblk(nsets * ngroups, 64)), dim3(64), 0, st, ws.segs, g, nsets * ngroups, ws.out2);
+  const uint32_t* rowsum = ws.runs;
+  if (g.nseg > 1)
+    hipLaunchKernelGGL(k_msm_rowtree28<C>, dim3(nblk(ngw * lpr, 256)), dim3(256), 0, st, ws.segs, g.nseg, ngw, lpr, span, ws.runs);
+  else
+    rowsum = ws.segs;  // one segment per row: its value is the row sum
+  if (g.nseg > 64) {
+    hipLaunchKernelGGL(k_msm_rowred28<C>, dim3((unsigned)ngw), dim3(64), 0, st, ws.runs, g.nseg / 64, ws.segs);
+    rowsum = ws.segs;
+  }
+  hipLaunchKernelGGL(k_msm_windows28<C>, dim3(nblk(nsets * ngroups, 64)), dim3(64), 0, st, rowsum, g, nsets * ngroups, ws.out2);
   return hipGetLastError();
 }
 

@@ -209,14 +209,24 @@ __global__ __launch_bounds__(64) void k_lambda(const uint32_t* __restrict__ key,
     }
     const fr dinv = fr_mul(inv, pk);
     inv = fr_mul(inv, dk);
-    uint32_t words[8], pos[8], neg[8];
+    uint32_t words[8], sw[8], pos[8], neg[8];
     fr_to_words(fr_mul(nk, dinv), words);
-    fr_naf_masks(words, pos, neg);
+    // the NAFs recode the shorter of lambda and r - lambda (digits negated for the latter): the chains skip the
+    // doublings above the highest digit, so a small +-lambda costs a short chain (fr_short)
+    const bool flip = fr_short(words, sw);
+    fr_naf_masks(sw, pos, neg);
     for (int w = 0; w < 8; w++) {
-      L[LAM_WORDS * k + w] = pos[w];
-      L[LAM_WORDS * k + 8 + w] = neg[w];
+      L[LAM_WORDS * k + w] = flip ? neg[w] : pos[w];
+      L[LAM_WORDS * k + 8 + w] = flip ? pos[w] : neg[w];
     }
-    fr_wnaf4(words, L + LAM_WORDS * k + 16);
+    uint32_t* nib = L + LAM_WORDS * k + 16;
+    fr_wnaf4(sw, nib);
+    if (flip)
+      for (int w = 0; w < 32; w++) {
+        // a nonzero nibble v (1..4 or 9..12) changes sign: v ^ 8
+        const uint32_t x = nib[w], nz = (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x11111111u;
+        nib[w] = x ^ (nz << 3);
+      }
     fr_reg4(words, L + LAM_WORDS * k + 48);
   }
 }

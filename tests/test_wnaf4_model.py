@@ -72,3 +72,27 @@ def test_reg4_digits():
             assert 1 <= mag <= 15
             total += (-mag if v & 8 else mag) * 16 ** i
         assert total % R == lam, lam
+
+
+def test_short_signed_wnaf4_of_first_subset():
+    """k_lambda (k_recover.hip) recodes the shorter of lambda and r - lambda (fr.hpp fr_short) and negates the digits of
+    the latter: the sum is lambda mod r, and for the first t signers (lambda_k = +-C(t, k) mod r, x = 1 .. t) every
+    coefficient's width-4 NAF ends below bit 32, so k_lagrange's chain skips the doublings above it."""
+    from math import comb
+    R = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    t = 33
+    for k in range(1, t + 1):
+        num = den = 1
+        for m in range(1, t + 1):
+            if m != k:
+                num = num * m % R
+                den = den * (m - k) % R
+        lam = num * pow(den, R - 2, R) % R
+        assert lam in (comb(t, k), R - comb(t, k))
+        flip = R - lam < lam
+        nib = wnaf4_nibbles(R - lam if flip else lam)
+        if flip:
+            nib = [v ^ 8 if v else 0 for v in nib]
+        total = sum((-(2 * (v & 7) - 1) if v & 8 else 2 * (v & 7) - 1) << b for b, v in enumerate(nib) if v)
+        assert total % R == lam
+        assert max(b for b, v in enumerate(nib) if v) < 32
