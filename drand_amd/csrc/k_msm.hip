@@ -507,13 +507,17 @@ __device__ __constant__ uint32_t BETA28[14] = {0xa75929au, 0x681b798u, 0x22a3e9d
 DH_DEV f28 c28_g1::endo_x(const f28& x) { return f28_mul(x, f28_c(BETA28)); }
 
 // The batch's points in the lazy affine form, each followed (index n + i) by its endomorphism image (phi on G1,
-// psi on G2; G2 also psi^2 and psi^3 at 2n + i and 3n + i, the four parts of its scalars): S from the decoded signatures; Q from the Jacobian hash points, made affine here with one
-// variable-time inversion per K rounds (Montgomery's trick: the prefix products of Z go to Q's x slots on the
-// way forward, each 1/Z comes out on the way back). The bucket pass then takes mixed additions for both point sets:
-// 7M + 4S per entry instead of 11M + 5S for the hash points, against ~8 (G1) / ~25 (G2) products per round here. A
-// hash point at infinity (Z = 0, probability ~2^-255) cannot be the message of a valid signature: its round is
-// marked DEC_BAD, which is its VerifyBeacon verdict. K (rounds per inversion) follows the batch size so that the
-// launch fills the chip's 2-wave residency (131,072 lanes): 8 at 1M rounds, 1 at a 131k shard (prep28_k).
+// psi on G2; G2 also psi^2 and psi^3 at 2n + i and 3n + i, the four parts of its scalars): S from the decoded
+// signatures; Q from the Jacobian hash points, made affine with ONE variable-time inversion per workgroup (Montgomery's
+// trick at two levels: each lane multiplies the Z's of its K rounds, storing the prefix products in Q's x slots; the
+// workgroup's 256 lane products are combined by a prefix and a suffix product scan through LDS, lane 0 inverts the
+// total, and each lane's inverse is total^-1 x (the other lanes' product); each 1/Z then comes out on the lane's way
+// back). The bucket pass takes mixed additions for both point sets: 7M + 4S per entry instead of 11M + 5S for the hash
+// points. A hash point at infinity (Z = 0, probability ~2^-255) cannot be the message of a valid signature: its round
+// is marked DEC_BAD, which is its VerifyBeacon verdict. K (rounds per lane) follows the batch size so that the launch
+// fills the chip's 2-wave residency (131,072 lanes): 8 at 1M rounds, 1 at a 131k shard (prep28_k). r04 inverted once
+// per lane: at a 131k shard (K = 1) that was one ~64k-instruction inversion per round, as much work per batch as a 1M
+// batch's, ~12% of the pipelined 131k shape's GPU time (profiles/r05/node_131072_trace_r05l).
 constexpr uint32_t PREP28_KMAX = 16;
 // the endomorphism images of affine point i at part * n + i
 template <class C>
@@ -534,6 +538,23 @@ static uint32_t prep28_k(size_t n) {
   while (k < PREP28_KMAX && n / (2 * k) >= 131072) k *= 2;
   return k;
 }
+// inclusive product scan of v over the workgroup's 256 lanes, forwards (lane t: v_0 ... v_t) or backwards (v_t ... v_255)
+template <class C, bool BACK>
+DH_DEV typename C::E block_product_scan(typename C::E v, typename C::E* sh) {
+  const int t = threadIdx.x;
+#pragma unroll 1
+  for (int off = 1; off < 256; off <<= 1) {
+    sh[t] = v;
+    __syncthreads();
+    const int src = BACK ? t + off : t - off;
+    const bool has = BACK ? src < 256 : src >= 0;
+    typename C::E o;
+    if (has) o = sh[src];
+    __syncthreads();
+    if (has) v = C::mulr(v, o);
+  }
+  return v;
+}
 // sets: bit 0 converts S (sig_aff), bit 1 Q (q_pts); tbls Recover converts its partials and its round hash points
 // separately (different counts)
 template <class C>
@@ -543,9 +564,9 @@ __global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint32_t K, uin
   using E = typename C::E;
   using F = typename C::F;
   constexpr int EW = C::EW, FW = npw<F>::N;
+  __shared__ E sh[256];
   const size_t lo = gtid() * K;
-  if (lo >= n) return;
-  const size_t hi = min(n, lo + K);
+  const size_t hi = lo < n ? min(n, lo + K) : lo;  // lanes past n take part in the workgroup's scans only
 #pragma unroll 1
   for (size_t i = lo; i < hi && (sets & 1); i++) {
     if (status[i] != DEC_OK) continue;
@@ -555,9 +576,8 @@ __global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint32_t K, uin
     st28(S + 2 * EW * i + EW, y, 0);
     prep28_images<C>(S, n, i, x, y);
   }
-  if (!(sets & 2)) return;
+  if (!(sets & 2)) return;  // a kernel argument: uniform, before the barriers
   E acc = C::one();
-  bool any = false;
 #pragma unroll 1
   for (size_t i = lo; i < hi; i++) {
     if (status[i] != DEC_OK) continue;
@@ -569,17 +589,30 @@ __global__ __launch_bounds__(256, 2) void k_msm_prep28(size_t n, uint32_t K, uin
     }
     st28(Q + 2 * EW * i, acc, 0);  // prefix product, read back below
     acc = C::mulr(acc, C::in(z));
-    any = true;
   }
-  if (!any) return;
-  E inv = C::inv(acc);
+  // acc^-1 = total^-1 x (product of the other lanes' acc): exclusive prefix x exclusive suffix
+  const int t = threadIdx.x;
+  const E pre = block_product_scan<C, false>(acc, sh);
+  sh[t] = pre;
+  __syncthreads();
+  const E pre_x = t ? sh[t - 1] : C::one();
+  __syncthreads();
+  if (t == 255) sh[0] = C::inv(pre);  // the workgroup's one inversion (every factor is a nonzero Z or one)
+  __syncthreads();
+  const E tinv = sh[0];
+  __syncthreads();
+  const E suf = block_product_scan<C, true>(acc, sh);
+  sh[t] = suf;
+  __syncthreads();
+  const E suf_x = t < 255 ? sh[t + 1] : C::one();
+  E inv = C::mulr(C::mulr(tinv, pre_x), suf_x);
 #pragma unroll 1
   for (size_t k = hi; k-- > lo;) {
     if (status[k] != DEC_OK) continue;
-    E pre;
-    ld28(pre, Q + 2 * EW * k);
+    E pr;
+    ld28(pr, Q + 2 * EW * k);
     const jac<F> q = ld_jac_aos<F>(q_pts, k);
-    const E zi = C::mulr(inv, pre);
+    const E zi = C::mulr(inv, pr);
     inv = C::mulr(inv, C::in(q.z));
     const E zi2 = C::sqrr(zi);
     const E x = C::mulr(C::in(q.x), zi2);
