@@ -253,10 +253,16 @@ struct lease {
   }
 };
 
-int set_device_and_stream(worker* w) {
+// The tail stream is created on a worker's first local call: a worker that only ever runs node batches (one stream
+// per batch) holds one stream. HIP hands a process's streams its hardware queues in creation order, round robin; with
+// two streams per worker, the node batches' streams landed on every other queue (8 of 16), so more than 8 batches in
+// flight doubled some queues up and not others, and the one host thread retiring batches in order waited on the
+// doubled ones: 131k-round node batches 21.5 M/s at 8-11 in flight, 16.3 at 12, 19.5 at 16 (19.8 at 12 over 8
+// queues, 16.7 at 8 over 4: profiles/r05/node_131072_sweep_r05k).
+int set_device_and_stream(worker* w, bool need_tail = true) {
   HIP_TRY(hipSetDevice(g_ctx.device));
   if (!w->stream) HIP_TRY(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
-  if (!w->tail) {
+  if (!w->tail && need_tail) {
     int least = 0, greatest = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIP_TRY(hipStreamCreateWithPriority(&w->tail, hipStreamNonBlocking, greatest));
@@ -1538,7 +1544,7 @@ int dh_batch_begin(int scheme, const uint8_t* pk, size_t pk_len, const uint64_t*
     return rc;
   }
   worker* w = b->L->w;
-  int rc = set_device_and_stream(w);
+  int rc = set_device_and_stream(w, !node_one_stream());
   if (!rc && hip_stream) {  // inputs produced on the caller's stream
     if (hipEventRecord(w->part_ready, (hipStream_t)hip_stream) != hipSuccess ||
         hipStreamWaitEvent(w->stream, w->part_ready, 0) != hipSuccess)
