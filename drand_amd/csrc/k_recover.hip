@@ -477,6 +477,7 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
   constexpr int JW = sizeof(F) / 4 * 3;
   __shared__ uint32_t part[(LG_LANES - 1) * 64 * JW];  // the partial sums of waves 1 .. LG_LANES - 1
   __shared__ uint32_t idxS[64 * LG_LANES][LG_MAXK], lpS[64 * LG_LANES][LG_MAXK], lnS[64 * LG_LANES][LG_MAXK];
+  __shared__ uint32_t accS[sizeof(F) == sizeof(fp2) ? 64 * LG_LANES * JW : 1];  // G2: the lanes' sums over passes
   const bool sliced = blockIdx.x >= full;
   const uint32_t r = blockIdx.x - full;
   const size_t blk = sliced ? full + r / S : blockIdx.x;
@@ -504,13 +505,21 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
       for (int i = 0; i < nc; i++) idx[i] = Sel[q + nl * (c0 + i)];
       if constexpr (sizeof(F) == sizeof(fp2)) {
         // width-4 NAF over the partials' tables; a chain that met an exceptional case (poisoned) runs again with
-        // the exact formulas
+        // the exact formulas. The running sum of the passes waits in the lane's LDS slot (accS), not in 72 registers
+        // live across the chain, which holds 512
         j228 a28 = regular ? lagrange_reg28<false>(L, q, nl, c0, nc, tbl, tw, idx, lp)
                            : lagrange_wnaf28<false>(L, q, nl, c0, nc, tbl, tw, idx, lp);
         if (j228_poisoned(a28))
           a28 = regular ? lagrange_reg28<true>(L, q, nl, c0, nc, tbl, tw, idx, lp)
                         : lagrange_wnaf28<true>(L, q, nl, c0, nc, tbl, tw, idx, lp);
-        if (!a28.inf) acc = jac_add(acc, jac<F>{f2_to_fp2(a28.x), f2_to_fp2(a28.y), f2_to_fp2(a28.z)});
+        if (!a28.inf) {
+          const jac<F> s{f2_to_fp2(a28.x), f2_to_fp2(a28.y), f2_to_fp2(a28.z)};
+          st_jac_aos<F>(accS, threadIdx.x, c0 ? jac_add(ld_jac_aos<F>(accS, threadIdx.x), s) : s);
+        } else if (!c0) {
+          st_jac_aos<F>(accS, threadIdx.x, jac_inf<F>());
+        }
+        asm volatile("" ::: "memory");  // the sum is reloaded from LDS, not kept in registers across the next chain
+        if (c0 + LG_MAXK >= nt) acc = ld_jac_aos<F>(accS, threadIdx.x);
         continue;
       }
       jac<F> part_acc = jac_inf<F>();
