@@ -407,6 +407,14 @@ size_t wnaf_table_scratch_bytes(size_t n, int entries) { return n * (size_t)(ent
 size_t lam_words() { return LAM_WORDS; }
 
 // the width-4 NAF Straus chain of one lane's terms over their tables (nibble words of the current 8 positions in nw)
+// a table entry's coordinates for j228_madd_ld, loaded where the formula uses them (k = 0: x, 1: y, negated for a
+// negative digit): the chain's mixed addition then holds neither coordinate across the products before its use
+DH_DEV auto entry_ld(const uint32_t* pt, bool neg) {
+  return [pt, neg](int k) {
+    const f228 c{ld_f28w(pt + 32 * k), ld_f28w(pt + 32 * k + 16)};
+    return k && neg ? f2_neg3(c) : c;
+  };
+}
 template <bool EXACT>
 DH_DEV j228 lagrange_wnaf28(const uint32_t* __restrict__ L, int q, int nl, int c0, int nc, const uint32_t* __restrict__ tbl,
                             uint32_t tw, const uint32_t* idx, uint32_t* nw) {
@@ -421,10 +429,7 @@ DH_DEV j228 lagrange_wnaf28(const uint32_t* __restrict__ L, int q, int nl, int c
       const uint32_t v = (nw[i] >> (4 * (b & 7))) & 15;
       if (v) {
         const uint32_t* pt = tbl + (size_t)tw * idx[i] + A28_WORDS * ((v & 7) - 1);
-        const f228 x{ld_f28w(pt), ld_f28w(pt + 16)};
-        f228 y{ld_f28w(pt + 32), ld_f28w(pt + 48)};
-        if (v & 8) y = f2_neg3(y);
-        acc = j228_madd<EXACT>(acc, x, y);
+        acc = j228_madd_ld<EXACT, false>(acc, entry_ld(pt, v & 8));
       }
     }
   }
@@ -452,10 +457,7 @@ DH_DEV j228 lagrange_reg28(const uint32_t* __restrict__ L, int q, int nl, int c0
     for (int i = 0; i < nc; i++) {
       const uint32_t v = (nw[i] >> (4 * (wi & 7))) & 15;
       const uint32_t* pt = tbl + (size_t)tw * idx[i] + A28_WORDS * (v & 7);
-      const f228 x{ld_f28w(pt), ld_f28w(pt + 16)};
-      f228 y{ld_f28w(pt + 32), ld_f28w(pt + 48)};
-      if (v & 8) y = f2_neg3(y);
-      acc = j228_madd<EXACT>(acc, x, y);
+      acc = j228_madd_ld<EXACT, false>(acc, entry_ld(pt, v & 8));
     }
   }
   return acc;
