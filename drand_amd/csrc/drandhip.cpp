@@ -1165,7 +1165,7 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     return dh::launch_select_lagrange(w->r_off.as<uint32_t>(), w->r_ok.as<uint8_t>(), w->r_pidx.as<uint32_t>(), t, n_rounds,
                                       w->r_sel.as<uint32_t>(), w->r_key.as<uint32_t>(), w->r_den.as<uint32_t>(),
                                       w->r_lam.as<uint32_t>(), w->r_lamset.as<uint32_t>(), w->r_rok.as<uint8_t>(),
-                                      w->r_own.as<uint32_t>(), st);
+                                      w->r_own.as<uint32_t>(), g2 ? 0 : 1, st);
   }));
   // tables of 8 odd multiples when some round has a Lagrange basis of its own (its wave then runs the regular windows
   // in k_lagrange), else of 4 for the width-4 NAF: one word back from the device

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(64) void k_select_lagrange(const uint32_t* __restri
 // lam_set[j] = j. lam_set is what k_lagrange reads.
 __global__ __launch_bounds__(64) void k_lambda(const uint32_t* __restrict__ key, const uint8_t* __restrict__ rok, int t,
                                                size_t n_rounds, uint32_t* __restrict__ den, uint32_t* __restrict__ lam,
-                                               uint32_t* __restrict__ lam_set, uint32_t* __restrict__ own) {
+                                               uint32_t* __restrict__ lam_set, uint32_t* __restrict__ own, int masks) {
   const size_t j = gtid();
   if (j >= n_rounds || !rok[j]) return;
   const uint32_t* K = key + j * (size_t)t;
@@ -180,20 +180,28 @@ __global__ __launch_bounds__(64) void k_lambda(const uint32_t* __restrict__ key,
   if (j > 0) atomicAdd(own, 1u);
   uint32_t* D = den + j * (size_t)t * 8;
   uint32_t* L = lam + j * (size_t)t * LAM_WORDS;
-  // pass 1: numerators (into lam's second half), denominators (scratch), prefix products (into lam's first half)
-  fr pre = fr_one();
+  // x_m in Montgomery form once per round, parked in each term's nibble words (written in pass 2, after the last use)
+  for (int m = 0; m < t; m++) {
+    const fr xm = fr_from_u32(K[m] + 1);
+    for (int w = 0; w < 8; w++) L[LAM_WORDS * m + 16 + w] = xm.v[w];
+  }
+  auto ldx = [&](int m) {
+    fr x;
+    for (int w = 0; w < 8; w++) x.v[w] = L[LAM_WORDS * m + 16 + w];
+    return x;
+  };
+  // pass 1: lambda_k = N / (x_k prod_{m != k} (x_m - x_k)) with N = prod_m x_m: the denominators (scratch) and their
+  // prefix products (into lam's first words); one product per (k, m) (r04 formed each numerator too and converted x_m
+  // to Montgomery form in the inner loop: three products per pair)
+  fr pre = fr_one(), N = fr_one();
   for (int k = 0; k < t; k++) {
-    const fr xk = fr_from_u32(K[k] + 1);
-    fr num = fr_one(), dk = fr_one();
-    for (int m = 0; m < t; m++) {
-      if (m == k) continue;
-      const fr xm = fr_from_u32(K[m] + 1);
-      num = fr_mul(num, xm);
-      dk = fr_mul(dk, fr_sub(xm, xk));
-    }
+    const fr xk = ldx(k);
+    N = fr_mul(N, xk);
+    fr dk = xk;
+    for (int m = 0; m < t; m++)
+      if (m != k) dk = fr_mul(dk, fr_sub(ldx(m), xk));
     for (int w = 0; w < 8; w++) {
       L[LAM_WORDS * k + w] = pre.v[w];
-      L[LAM_WORDS * k + 8 + w] = num.v[w];
       D[8 * k + w] = dk.v[w];
     }
     pre = fr_mul(pre, dk);
@@ -201,23 +209,24 @@ __global__ __launch_bounds__(64) void k_lambda(const uint32_t* __restrict__ key,
   // pass 2: one inversion of the product, then lambda_k from the back
   fr inv = fr_inv(pre);
   for (int k = t - 1; k >= 0; k--) {
-    fr pk, nk, dk;
+    fr pk, dk;
     for (int w = 0; w < 8; w++) {
       pk.v[w] = L[LAM_WORDS * k + w];
-      nk.v[w] = L[LAM_WORDS * k + 8 + w];
       dk.v[w] = D[8 * k + w];
     }
     const fr dinv = fr_mul(inv, pk);
     inv = fr_mul(inv, dk);
     uint32_t words[8], sw[8], pos[8], neg[8];
-    fr_to_words(fr_mul(nk, dinv), words);
+    fr_to_words(fr_mul(N, dinv), words);
     // the NAFs recode the shorter of lambda and r - lambda (digits negated for the latter): the chains skip the
     // doublings above the highest digit, so a small +-lambda costs a short chain (fr_short)
     const bool flip = fr_short(words, sw);
-    fr_naf_masks(sw, pos, neg);
-    for (int w = 0; w < 8; w++) {
-      L[LAM_WORDS * k + w] = flip ? neg[w] : pos[w];
-      L[LAM_WORDS * k + 8 + w] = flip ? pos[w] : neg[w];
+    if (masks) {  // the G1 chain's NAF digit masks (G2 reads the nibbles)
+      fr_naf_masks(sw, pos, neg);
+      for (int w = 0; w < 8; w++) {
+        L[LAM_WORDS * k + w] = flip ? neg[w] : pos[w];
+        L[LAM_WORDS * k + 8 + w] = flip ? pos[w] : neg[w];
+      }
     }
     uint32_t* nib = L + LAM_WORDS * k + 16;
     fr_wnaf4(sw, nib);
@@ -306,12 +315,14 @@ DH_DEV void st_f28w(uint32_t* p, const f28& a) {
 }
 // G2 table per valid partial: the odd multiples P, 3P, ..., (2 NE - 1) P affine in the 28-bit form (NE x 64 words):
 // NE = 4 for the width-4 NAF chains (digits up to 7), NE = 8 when some wave's rounds do not share one Lagrange basis and
-// run the regular 4-bit windows (digits up to 15). The Jacobian Z's of all the lane's entries (TB_K partials x NE - 1)
-// share one variable-time Fp2 inversion by Montgomery's trick (r04d spent 30.6 ms on 3.3M tables with one inversion
-// per partial): each Z and the product of the lane's Z's before it are parked in zs, X and Y in their table slots,
-// and the walk back after the inversion turns each entry affine. The partials reaching k_lagrange decoded to subgroup
-// points, so the multiples are finite and distinct from the points added to them: the exact formulas only guard the
-// table of a partial that is never selected.
+// run the regular 4-bit windows (digits up to 15). The multiples come from co-Z additions (Meloni's ZADDU, the
+// odd-multiples chain of Longa and Gebotys): 2P and P share a Z after the doubling (DBLU from affine P, 2M + 4S), and
+// each (2j + 1) P = 2P + (2j - 1) P is one ZADDU (5M + 2S) that also returns 2P on the new Z, so the entries' Z's
+// differ only by the factors d_j = X(2P) - X((2j - 1) P): Z_j = Z_{j-1} d_j. r04 took a doubling, a mixed and NE - 2
+// full Jacobian additions (16M + ... each) and normalised every entry's own Z. Now each partial contributes ONE Z (its
+// last entry's) to the lane's Montgomery chain over its TB_K partials (one variable-time Fp2 inversion per lane), and
+// the walk back turns 1/Z_last into every 1/Z_j by the parked d_j's. The partials reaching k_lagrange decoded to
+// subgroup points (order r), so 2P is never +-(2j - 1) P and no co-Z step meets an exceptional case.
 constexpr int TB_K = 8;
 DH_DEV void st_f228w(uint32_t* p, const f228& a) {
   st_f28w(p, a.c0);
@@ -321,7 +332,9 @@ DH_DEV f228 ld_f228w(const uint32_t* p) { return f228{ld_f28w(p), ld_f28w(p + 16
 template <int NE>
 __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restrict__ paff, const uint8_t* __restrict__ ok,
                                                        size_t n, uint32_t* __restrict__ tbl, uint32_t* __restrict__ zs) {
-  constexpr size_t TW = (size_t)NE * A28_WORDS, ZW = (size_t)(NE - 1) * 64;  // words per partial: table, scratch
+  // words per partial: table; scratch d_1 .. d_{NE-1}, Z_last, the product of the lane's earlier Z_last's (32 each)
+  constexpr size_t TW = (size_t)NE * A28_WORDS, ZW = (size_t)(NE - 1) * 64;
+  static_assert((NE + 1) * 32 <= ZW, "co-Z scratch");
   const size_t nth = (n + TB_K - 1) / TB_K;
   const size_t t = gtid();
   if (t >= nth) return;
@@ -339,22 +352,41 @@ __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restric
     uint32_t* z = zs + ZW * e;
     st_f228w(o, px);
     st_f228w(o + 32, py);
-    const j228 two = j228_dbl(j228{px, py, f2_one(), false});
-    j228 m = j228_madd<true>(two, px, py);  // 3P
+    // DBLU: 2P = (M^2 - 2S, M (S - X2) - 8B^2, 2y) and P on the same Z = (S, 8B^2), B = y^2, S = 4xB, M = 3x^2
+    // (bounds in units of p per component; every stored value reduced below 2)
+    const f228 B = f2_red(f2_sqr<2>(py));
+    const f228 S = f2_red(f2_scale(f2_red(f2_mul(px, B)), 4));
+    const f228 M = f2_scale(f2_red(f2_sqr<2>(px)), 3);                                    // < 6
+    f228 tx = f2_red(f2_lin<4, 4>(f2_sqr<6>(M), 1, S, -2));                               // (2, 4) + 4p - 2S
+    const f228 e8 = f2_red(f2_scale(f2_red(f2_sqr<2>(B)), 8));                             // 8B^2
+    f228 ty = f2_red(f2_lin<2, 2>(f2_mul(M, f2_lin<2, 2>(S, 1, tx, -1)), 1, e8, -1));     // 6 x 4 -> (4, 6) + 2p - 8B^2
+    f228 zl = f2_red(f2_scale(py, 2));                                                      // Z of 2P and P
+    f228 rx = S, ry = e8;
 #pragma unroll 1
     for (int j = 1; j < NE; j++) {
-      if (j > 1) m = j228_add<true>(m, two);  // (2j + 1) P
+      // ZADDU(T = 2P, R = (2j - 1) P): R' = T + R, T' = T, both on Z d
+      const f228 d = f2_lin<2, 2>(tx, 1, rx, -1);                                         // < 4
+      const f228 C = f2_red(f2_sqr<4>(d));
+      const f228 w1 = f2_red(f2_mul(tx, C)), w2 = f2_red(f2_mul(rx, C));
+      const f228 ee = f2_lin<2, 2>(ty, 1, ry, -1);                                        // < 4
+      const f228 a1 = f2_red(f2_mul(ty, f2_lin<2, 2>(w1, 1, w2, -1)));
+      rx = f2_red(f2_lin3<4, 4>(f2_sqr<4>(ee), 1, w1, -1, w2, -1));                       // (2, 4) + 4p - W1 - W2
+      ry = f2_red(f2_lin<2, 2>(f2_mul(ee, f2_lin<2, 2>(w1, 1, rx, -1)), 1, a1, -1));      // 4 x 4 -> (4, 6) + 2p - A1
+      tx = w1;
+      ty = a1;
+      zl = f2_red(f2_mul(zl, d));
+      st_f228w(z + 32 * (j - 1), f2_red(d));
       uint32_t* sl = o + A28_WORDS * j;
-      st_f228w(sl, m.x);
-      st_f228w(sl + 32, m.y);
-      st_f228w(z + 64 * (j - 1), m.z);
-      if (any) st_f228w(z + 64 * (j - 1) + 32, pre);  // the product of the lane's Z's before this one
-      pre = any ? f2_red(f2_mul(pre, m.z)) : m.z;
-      any = true;
+      st_f228w(sl, rx);
+      st_f228w(sl + 32, ry);
     }
+    st_f228w(z + 32 * (NE - 1), zl);
+    if (any) st_f228w(z + 32 * NE, pre);  // the product of the lane's Z_last's before this one
+    pre = any ? f2_red(f2_mul(pre, zl)) : zl;
+    any = true;
   }
   if (!any) return;
-  f228 inv = f2_from_fp2(fp2_inv_vt(f2_to_fp2(pre)));  // 1 / (product of every Z of the lane)
+  f228 inv = f2_from_fp2(fp2_inv_vt(f2_to_fp2(pre)));  // 1 / (product of the lane's Z_last's)
 #pragma unroll 1
   for (int k = TB_K - 1; k >= 0; k--) {
     if (!(valid >> k & 1)) continue;
@@ -362,19 +394,19 @@ __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restric
     const uint32_t* z = zs + ZW * e;
     uint32_t* o = tbl + TW * e;
     const bool earlier = (valid & ((1u << k) - 1)) != 0;  // a valid partial before this one in the lane
+    // 1 / Z_last: inv for the lane's first partial, else inv * (product before it); inv moves past Z_last
+    f228 zi = inv;
+    if (earlier) {
+      zi = f2_red(f2_mul(inv, ld_f228w(z + 32 * NE)));
+      inv = f2_red(f2_mul(inv, ld_f228w(z + 32 * (NE - 1))));
+    }
 #pragma unroll 1
     for (int j = NE - 1; j >= 1; j--) {
-      // the lane's first Z: inv is its inverse; otherwise inv * (product before it), and inv moves past it
-      const bool later = earlier || j > 1;
-      f228 zi = inv;
-      if (later) {
-        zi = f2_red(f2_mul(inv, ld_f228w(z + 64 * (j - 1) + 32)));
-        inv = f2_red(f2_mul(inv, ld_f228w(z + 64 * (j - 1))));
-      }
       uint32_t* sl = o + A28_WORDS * j;
       const f228 z2 = f2_red(f2_sqr<2>(zi));
       st_f228w(sl, f2_red(f2_mul(ld_f228w(sl), z2)));
       st_f228w(sl + 32, f2_red(f2_mul(ld_f228w(sl + 32), f2_red(f2_mul(z2, zi)))));
+      if (j > 1) zi = f2_red(f2_mul(zi, ld_f228w(z + 32 * (j - 1))));  // 1 / Z_{j-1} = d_j / Z_j
     }
   }
 }
@@ -672,13 +704,13 @@ hipError_t launch_ok_from_status(const uint8_t* status, size_t np, uint8_t* ok, 
 
 hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const uint32_t* share_idx, int t, size_t n_rounds,
                                   uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint32_t* lam_set, uint8_t* rok,
-                                  uint32_t* own, hipStream_t st) {
+                                  uint32_t* own, int g1, hipStream_t st) {
   if (!n_rounds) return hipSuccess;
   hipError_t e = hipMemsetAsync(own, 0, 4, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_select_lagrange, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, off, ok, share_idx, t, n_rounds, sel, key,
                      rok);
-  hipLaunchKernelGGL(k_lambda, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, key, rok, t, n_rounds, den, lam, lam_set, own);
+  hipLaunchKernelGGL(k_lambda, dim3(nblk(n_rounds, 64)), dim3(64), 0, st, key, rok, t, n_rounds, den, lam, lam_set, own, g1);
   return hipGetLastError();
 }
 

@@ -154,7 +154,7 @@ hipError_t launch_ok_from_status(const uint8_t* status, size_t np, uint8_t* ok, 
 size_t lam_words();
 hipError_t launch_select_lagrange(const uint32_t* off, const uint8_t* ok, const uint32_t* share_idx, int t, size_t n_rounds,
                                   uint32_t* sel, uint32_t* key, uint32_t* den, uint32_t* lam, uint32_t* lam_set, uint8_t* rok,
-                                  uint32_t* own, hipStream_t st);
+                                  uint32_t* own, int g1, hipStream_t st);
 // tbl (G2): per valid partial (ok) the odd multiples P, 3P, ..., (2 entries - 1) P affine 28-bit (entries = 4 or 8,
 // 64 words each) from the partials' affine points (12 x 32-bit AOS); zs: wnaf_table_scratch_bytes(n, entries) of
 // scratch (the batched inversion's Z's); unused for G1
