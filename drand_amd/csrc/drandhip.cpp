@@ -439,7 +439,7 @@ static void fit_segments(dh::msm_geom& g, size_t ngroups, size_t nsets) {
   const size_t rows = std::max<size_t>(1, nsets * ngroups * (size_t)g.nwin);
   const size_t want = ((size_t)1 << 18) / rows + 1;
   size_t nseg = std::max<size_t>(1, std::min<size_t>({want, (size_t)g.nseg}));
-  if (nseg > 64) nseg &= ~(size_t)63;  // whole waves per row beyond 64 segments (k_msm.hip k_msm_segred28)
+  if (nseg > 512) nseg &= ~(size_t)511;  // rows of more than 64 lanes of 8 segments fill whole waves (k_msm_rowtree28)
   g.nseg = (uint32_t)nseg;
   g.seglen = (g.nbuck - 1 + g.nseg - 1) / g.nseg;
 }

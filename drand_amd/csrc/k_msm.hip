@@ -299,10 +299,14 @@ hipError_t launch_msm_sort(const msm_geom& g, const uint32_t* pidx, const uint32
   hipError_t e = hipMemsetAsync(ws.cnt, 0, nk * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   // DRANDHIP_SORT_GLOBAL=1 (experiments): the one-global-atomic-per-digit sort
-  static const bool global_sort = [] {
+  static const bool global_env = [] {
     const char* v = getenv("DRANDHIP_SORT_GLOBAL");
     return v && atoi(v) == 1;
   }();
+  // a tile whose keys span more than 16 slabs (a grouping by grp over many groups: the tbls per-signer sums at c = 16,
+  // 64 groups x 2 windows x 32,769 keys = 114 slabs) would be read once per slab: there the one-atomic-per-digit sort wins
+  // (k_msm_hist + k_msm_scatter 7.0 ms against 14.4 for the LDS sort, gpurun_out r05w)
+  const bool global_sort = global_env || (grp && nk > 16 * (size_t)SLAB_MAX);
   // the LDS sort's plan: tiles of about density x the slab's keys in digits (DRANDHIP_SORT_DENSITY), slabs of at
   // most SLAB_MAX keys over the keys a tile can touch
   dim3 grid;
@@ -811,7 +815,7 @@ DH_DEV typename C::P wave_tree(typename C::P acc, uint32_t* buf, uint32_t span) 
   const int nthr = blockDim.x, i = threadIdx.x, lane = i & 63;
 #pragma unroll 1
   for (uint32_t step = 1; step < span; step <<= 1) {
-    lds_put_pt<C>(buf, nthr, i, acc);
+    if ((lane & (2 * step - 1)) == step) lds_put_pt<C>(buf, nthr, i, acc);  // only the lanes read at this step
     __syncthreads();
     if ((lane & (2 * step - 1)) == 0) {
       typename C::P s = add_lds<C, false>(acc, buf, nthr, i + (int)step);
@@ -866,22 +870,36 @@ __global__ __launch_bounds__(256, C::OCC) void k_msm_segoff28(msm_geom g, size_t
 }
 
 // The segment values of a (set, group, window) row summed by wave-level trees through LDS (r04: a tree of log2(nseg)
-// launches of one addition per thread, 12 at level 0). k_msm_rowtree28: a row's nseg values sit on lpr lanes (nseg
-// rounded up to a power of two, the extra lanes holding the identity) when nseg <= 64, and wave_tree leaves the row sum
-// in its first lane; a longer row (a multiple of 64 segments: geom_for, fit_segments) covers whole waves, each leaving
-// one partial, and k_msm_rowred28 (one wave per row) sums the row's nseg / 64 partials the same way.
+// launches of one addition per thread, 12 at level 0). A tree inside a wave keeps few lanes busy (63 additions over 6
+// steps of 64 lanes), so k_msm_rowtree28 first has each lane add G consecutive segment values in a serial run (G = 8
+// for many rows of more than 64 segments: 7/8 of the additions at full lane use; 2 for level 0's few rows, whose
+// latency the one call waits on), then the wave tree sums the lanes: a
+// row's lanes (lpr = nseg / G, rounded up to a power of two <= 64 with the extra lanes holding the identity) leave the
+// row sum in its first lane, or, for more than 64 lanes (a multiple of 64: fit_segments), one partial per wave that
+// k_msm_rowred28 (one wave per row) sums the same way. Measured against r04's launch tree on the tbls MSMs (64 groups of
+// 2 windows of 2,048 segments, gpurun_out r05w): the pure wave tree was 8.2 ms against 4.4.
 template <class C>
-__global__ __launch_bounds__(256, C::OCC) void k_msm_rowtree28(const uint32_t* __restrict__ segs, uint32_t nseg, size_t ngw,
-                                                               uint32_t lpr, uint32_t span, uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(256, C::OCC) void k_msm_rowtree28(const uint32_t* __restrict__ segs, uint32_t nseg, uint32_t G,
+                                                               size_t ngw, uint32_t lpr, uint32_t span, uint32_t* __restrict__ out) {
   __shared__ uint32_t buf[lds_words<C>() * 256];
   const size_t t = gtid();
   typename C::P acc = C::inf();
-  if (t < ngw * lpr && t % lpr < nseg) acc = ldj28<C>(segs, (t / lpr) * nseg + t % lpr);
+  if (t < ngw * lpr) {
+    const size_t row = t / lpr;
+    const uint32_t s0 = (uint32_t)(t % lpr) * G;
+#pragma unroll 1
+    for (uint32_t k = s0; k < s0 + G && k < nseg; k++) {
+      const uint32_t* p = segs + (size_t)3 * C::EW * (row * nseg + k);
+      const typename C::P sum = C::template add_mem<false>(acc, p);
+      acc = C::poisoned(sum) ? C::template add_mem<true>(acc, p) : sum;
+    }
+  }
   acc = wave_tree<C>(acc, buf, span);
   if (t < ngw * lpr && (t & (span - 1)) == 0) stj28<C>(out, t / span, acc);
 }
 template <class C>
-__global__ __launch_bounds__(64) void k_msm_rowred28(const uint32_t* __restrict__ parts_in, uint32_t parts, uint32_t* __restrict__ rowsum) {
+__global__ __launch_bounds__(64) void k_msm_rowred28(const uint32_t* __restrict__ parts_in, uint32_t parts, uint32_t span,
+                                                     uint32_t* __restrict__ rowsum) {
   __shared__ uint32_t buf[lds_words<C>() * 64];
   const size_t row = blockIdx.x;
   typename C::P acc = C::inf();
@@ -890,7 +908,7 @@ __global__ __launch_bounds__(64) void k_msm_rowred28(const uint32_t* __restrict_
     const typename C::P s = C::template add_mem<false>(acc, p);
     acc = C::poisoned(s) ? C::template add_mem<true>(acc, p) : s;
   }
-  acc = wave_tree<C>(acc, buf, 64);
+  acc = wave_tree<C>(acc, buf, span);
   if (threadIdx.x == 0) stj28<C>(rowsum, row, acc);
 }
 
@@ -958,25 +976,34 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     }
   }
   const size_t rows = ngroups * g.nwin, ngw = (size_t)nsets * rows;
-  if (g.nseg > 64 && g.nseg % 64) return hipErrorInvalidValue;  // whole waves per row (geom_for, fit_segments)
   hipLaunchKernelGGL(k_msm_segsum28<C>, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs,
                      ws.runs);
   if (g.nseg > 1)
     hipLaunchKernelGGL(k_msm_segoff28<C>, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, g, ngw, ws.segs, ws.runs);
-  // row sums: ws.runs (free after the offsets) for nseg <= 64; else the waves' partials go to ws.runs and the row sums
-  // to ws.segs
-  uint32_t lpr = g.nseg, span = 64;
-  if (g.nseg <= 64) {
-    for (lpr = 1; lpr < g.nseg;) lpr *= 2;
-    span = lpr;
+  // row sums: ws.runs (free after the offsets) when a row's lanes fit one wave; else the waves' partials go to ws.runs
+  // and the row sums to ws.segs
+  // G: 8 when the rows' segments are many (the additions' count matters: the bisection's and the tbls per-signer
+  // levels), 2 when they are few (level 0: 4-8 rows, where the serial run lengthens the one call's latency path)
+  uint32_t G = g.nseg <= 64 ? 1 : (ngw * g.nseg >= ((size_t)1 << 17) ? 8 : 2);
+  if (G == 2 && g.nseg / 2 > 64 && (g.nseg / 2) % 64) G = 8;
+  uint32_t lpr = (g.nseg + G - 1) / G, span = 64;
+  if (lpr <= 64) {
+    for (span = 1; span < lpr;) span *= 2;
+    lpr = span;
+  } else if (lpr % 64) {
+    return hipErrorInvalidValue;  // fit_segments: rows of more than 512 segments hold a multiple of 512
   }
   const uint32_t* rowsum = ws.runs;
   if (g.nseg > 1)
-    hipLaunchKernelGGL(k_msm_rowtree28<C>, dim3(nblk(ngw * lpr, 256)), dim3(256), 0, st, ws.segs, g.nseg, ngw, lpr, span, ws.runs);
+    hipLaunchKernelGGL(k_msm_rowtree28<C>, dim3(nblk(ngw * lpr, 256)), dim3(256), 0, st, ws.segs, g.nseg, G, ngw, lpr, span,
+                       ws.runs);
   else
     rowsum = ws.segs;  // one segment per row: its value is the row sum
-  if (g.nseg > 64) {
-    hipLaunchKernelGGL(k_msm_rowred28<C>, dim3((unsigned)ngw), dim3(64), 0, st, ws.runs, g.nseg / 64, ws.segs);
+  if (lpr > 64) {
+    const uint32_t parts = lpr / 64;
+    uint32_t pspan = 1;
+    while (pspan < parts) pspan *= 2;
+    hipLaunchKernelGGL(k_msm_rowred28<C>, dim3((unsigned)ngw), dim3(64), 0, st, ws.runs, parts, pspan, ws.segs);
     rowsum = ws.segs;
   }
   hipLaunchKernelGGL(k_msm_windows28<C>, dim3(nblk(nsets * ngroups, 64)), dim3(64), 0, st, rowsum, g, nsets * ngroups, ws.out2);
