@@ -228,14 +228,19 @@ __global__ __launch_bounds__(64) void k_lambda(const uint32_t* __restrict__ key,
         L[LAM_WORDS * k + 8 + w] = flip ? pos[w] : neg[w];
       }
     }
-    uint32_t* nib = L + LAM_WORDS * k + 16;
-    fr_wnaf4(sw, nib);
-    if (flip)
-      for (int w = 0; w < 32; w++) {
-        // a nonzero nibble v (1..4 or 9..12) changes sign: v ^ 8
-        const uint32_t x = nib[w], nz = (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x11111111u;
-        nib[w] = x ^ (nz << 3);
-      }
+    if (masks) continue;  // G1 chains read the NAF masks only
+    // G2: the width-4 NAF for round 0's basis, which coherent waves share (k_lagrange runs every other basis on the
+    // regular windows); the regular digits for every basis
+    if (j == 0) {
+      uint32_t* nib = L + LAM_WORDS * k + 16;
+      fr_wnaf4(sw, nib);
+      if (flip)
+        for (int w = 0; w < 32; w++) {
+          // a nonzero nibble v (1..4 or 9..12) changes sign: v ^ 8
+          const uint32_t x = nib[w], nz = (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x11111111u;
+          nib[w] = x ^ (nz << 3);
+        }
+    }
     fr_reg4(words, L + LAM_WORDS * k + 48);
   }
 }
@@ -525,7 +530,9 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
   const uint32_t myset = live ? (lam_set ? lam_set[j] : (uint32_t)j) : 0xffffffffu;
   const unsigned long long act = __ballot(live);
   const uint32_t ref = __shfl(myset, act ? __ffsll((long long)act) - 1 : 0);
-  const bool regular = reg && !__all(!live || myset == ref);
+  // (a wave coherent on a basis other than round 0's runs the regular windows too: k_lambda writes the width-4 NAF
+  // nibbles for round 0's basis only)
+  const bool regular = reg && (!__all(!live || myset == ref) || ref != 0);
   if (live) {
     const uint32_t* L = lam + (lam_set ? (size_t)lam_set[j] : j) * t * LAM_WORDS;  // per term: NAF masks, wNAF nibbles
     const uint32_t* Sel = sel + j * (size_t)t;
