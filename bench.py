@@ -48,8 +48,9 @@ R_ORDER = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=24)
-    ap.add_argument("--warmup", type=int, default=8)
+    # 200 steps: ~8 s of timed GPU work at 1M rounds per step, long enough for an outside utilisation sampler
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--total-rounds", type=int, default=0,
                     help="strong scaling: one chain of this many rounds split over the GPUs")
     ap.add_argument("--rounds-per-gpu", type=int, default=0,

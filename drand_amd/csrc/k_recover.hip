@@ -359,27 +359,27 @@ __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restric
     st_f228w(o + 32, py);
     // DBLU: 2P = (M^2 - 2S, M (S - X2) - 8B^2, 2y) and P on the same Z = (S, 8B^2), B = y^2, S = 4xB, M = 3x^2
     // (bounds in units of p per component; every stored value reduced below 2)
-    const f228 B = f2_red(f2_sqr<2>(py));
-    const f228 S = f2_red(f2_scale(f2_red(f2_mul(px, B)), 4));
-    const f228 M = f2_scale(f2_red(f2_sqr<2>(px)), 3);                                    // < 6
-    f228 tx = f2_red(f2_lin<4, 4>(f2_sqr<6>(M), 1, S, -2));                               // (2, 4) + 4p - 2S
-    const f228 e8 = f2_red(f2_scale(f2_red(f2_sqr<2>(B)), 8));                             // 8B^2
-    f228 ty = f2_red(f2_lin<2, 2>(f2_mul(M, f2_lin<2, 2>(S, 1, tx, -1)), 1, e8, -1));     // 6 x 4 -> (4, 6) + 2p - 8B^2
+    const f228 B = f2_red(f2_sqr<2, true>(py));
+    const f228 S = f2_red(f2_scale(f2_red(f2_mul<true>(px, B)), 4));
+    const f228 M = f2_scale(f2_red(f2_sqr<2, true>(px)), 3);                                    // < 6
+    f228 tx = f2_red(f2_lin<4, 4>(f2_sqr<6, true>(M), 1, S, -2));                               // (2, 4) + 4p - 2S
+    const f228 e8 = f2_red(f2_scale(f2_red(f2_sqr<2, true>(B)), 8));                             // 8B^2
+    f228 ty = f2_red(f2_lin<2, 2>(f2_mul<true>(M, f2_lin<2, 2>(S, 1, tx, -1)), 1, e8, -1));     // 6 x 4 -> (4, 6) + 2p - 8B^2
     f228 zl = f2_red(f2_scale(py, 2));                                                      // Z of 2P and P
     f228 rx = S, ry = e8;
 #pragma unroll 1
     for (int j = 1; j < NE; j++) {
       // ZADDU(T = 2P, R = (2j - 1) P): R' = T + R, T' = T, both on Z d
       const f228 d = f2_lin<2, 2>(tx, 1, rx, -1);                                         // < 4
-      const f228 C = f2_red(f2_sqr<4>(d));
-      const f228 w1 = f2_red(f2_mul(tx, C)), w2 = f2_red(f2_mul(rx, C));
+      const f228 C = f2_red(f2_sqr<4, true>(d));
+      const f228 w1 = f2_red(f2_mul<true>(tx, C)), w2 = f2_red(f2_mul<true>(rx, C));
       const f228 ee = f2_lin<2, 2>(ty, 1, ry, -1);                                        // < 4
-      const f228 a1 = f2_red(f2_mul(ty, f2_lin<2, 2>(w1, 1, w2, -1)));
-      rx = f2_red(f2_lin3<4, 4>(f2_sqr<4>(ee), 1, w1, -1, w2, -1));                       // (2, 4) + 4p - W1 - W2
-      ry = f2_red(f2_lin<2, 2>(f2_mul(ee, f2_lin<2, 2>(w1, 1, rx, -1)), 1, a1, -1));      // 4 x 4 -> (4, 6) + 2p - A1
+      const f228 a1 = f2_red(f2_mul<true>(ty, f2_lin<2, 2>(w1, 1, w2, -1)));
+      rx = f2_red(f2_lin3<4, 4>(f2_sqr<4, true>(ee), 1, w1, -1, w2, -1));                       // (2, 4) + 4p - W1 - W2
+      ry = f2_red(f2_lin<2, 2>(f2_mul<true>(ee, f2_lin<2, 2>(w1, 1, rx, -1)), 1, a1, -1));      // 4 x 4 -> (4, 6) + 2p - A1
       tx = w1;
       ty = a1;
-      zl = f2_red(f2_mul(zl, d));
+      zl = f2_red(f2_mul<true>(zl, d));
       st_f228w(z + 32 * (j - 1), f2_red(d));
       uint32_t* sl = o + A28_WORDS * j;
       st_f228w(sl, rx);
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restric
     }
     st_f228w(z + 32 * (NE - 1), zl);
     if (any) st_f228w(z + 32 * NE, pre);  // the product of the lane's Z_last's before this one
-    pre = any ? f2_red(f2_mul(pre, zl)) : zl;
+    pre = any ? f2_red(f2_mul<true>(pre, zl)) : zl;
     any = true;
   }
   if (!any) return;
@@ -402,16 +402,16 @@ __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restric
     // 1 / Z_last: inv for the lane's first partial, else inv * (product before it); inv moves past Z_last
     f228 zi = inv;
     if (earlier) {
-      zi = f2_red(f2_mul(inv, ld_f228w(z + 32 * NE)));
-      inv = f2_red(f2_mul(inv, ld_f228w(z + 32 * (NE - 1))));
+      zi = f2_red(f2_mul<true>(inv, ld_f228w(z + 32 * NE)));
+      inv = f2_red(f2_mul<true>(inv, ld_f228w(z + 32 * (NE - 1))));
     }
 #pragma unroll 1
     for (int j = NE - 1; j >= 1; j--) {
       uint32_t* sl = o + A28_WORDS * j;
-      const f228 z2 = f2_red(f2_sqr<2>(zi));
-      st_f228w(sl, f2_red(f2_mul(ld_f228w(sl), z2)));
-      st_f228w(sl + 32, f2_red(f2_mul(ld_f228w(sl + 32), f2_red(f2_mul(z2, zi)))));
-      if (j > 1) zi = f2_red(f2_mul(zi, ld_f228w(z + 32 * (j - 1))));  // 1 / Z_{j-1} = d_j / Z_j
+      const f228 z2 = f2_red(f2_sqr<2, true>(zi));
+      st_f228w(sl, f2_red(f2_mul<true>(ld_f228w(sl), z2)));
+      st_f228w(sl + 32, f2_red(f2_mul<true>(ld_f228w(sl + 32), f2_red(f2_mul<true>(z2, zi)))));
+      if (j > 1) zi = f2_red(f2_mul<true>(zi, ld_f228w(z + 32 * (j - 1))));  // 1 / Z_{j-1} = d_j / Z_j
     }
   }
 }
@@ -460,13 +460,13 @@ DH_DEV j228 lagrange_wnaf28(const uint32_t* __restrict__ L, int q, int nl, int c
   for (int b = 255; b >= 0; b--) {
     if ((b & 7) == 7)
       for (int i = 0; i < nc; i++) nw[i] = L[(size_t)(q + nl * (c0 + i)) * LAM_WORDS + 16 + (b >> 3)];
-    if (!acc.inf) acc = j228_dbl(acc);
+    if (!acc.inf) acc = j228_dbl<true>(acc);
 #pragma unroll 1
     for (int i = 0; i < nc; i++) {
       const uint32_t v = (nw[i] >> (4 * (b & 7))) & 15;
       if (v) {
         const uint32_t* pt = tbl + (size_t)tw * idx[i] + A28_WORDS * ((v & 7) - 1);
-        acc = j228_madd_ld<EXACT, false>(acc, entry_ld(pt, v & 8));
+        acc = j228_madd_ld<EXACT, true>(acc, entry_ld(pt, v & 8));
       }
     }
   }
@@ -488,13 +488,13 @@ DH_DEV j228 lagrange_reg28(const uint32_t* __restrict__ L, int q, int nl, int c0
       for (int i = 0; i < nc; i++) nw[i] = L[(size_t)(q + nl * (c0 + i)) * LAM_WORDS + 48 + (wi >> 3)];
     if (!acc.inf) {
 #pragma unroll 1
-      for (int d = 0; d < 4; d++) acc = j228_dbl(acc);
+      for (int d = 0; d < 4; d++) acc = j228_dbl<true>(acc);
     }
 #pragma unroll 1
     for (int i = 0; i < nc; i++) {
       const uint32_t v = (nw[i] >> (4 * (wi & 7))) & 15;
       const uint32_t* pt = tbl + (size_t)tw * idx[i] + A28_WORDS * (v & 7);
-      acc = j228_madd_ld<EXACT, false>(acc, entry_ld(pt, v & 8));
+      acc = j228_madd_ld<EXACT, true>(acc, entry_ld(pt, v & 8));
     }
   }
   return acc;
