@@ -363,7 +363,8 @@ __global__ __launch_bounds__(256) void k_wnaf_table_g2(const uint32_t* __restric
     const f228 S = f2_red(f2_scale(f2_red(f2_mul<true>(px, B)), 4));
     const f228 M = f2_scale(f2_red(f2_sqr<2, true>(px)), 3);                                    // < 6
     f228 tx = f2_red(f2_lin<4, 4>(f2_sqr<6, true>(M), 1, S, -2));                               // (2, 4) + 4p - 2S
-    const f228 e8 = f2_red(f2_scale(f2_red(f2_sqr<2, true>(B)), 8));                             // 8B^2
+    // 8B^2: the scale's limb sums 8 (2^28 - 1) + a carry <= 7 stay inside int32 (f28_lin)
+    const f228 e8 = f2_red(f2_scale(f2_red(f2_sqr<2, true>(B)), 8));
     f228 ty = f2_red(f2_lin<2, 2>(f2_mul<true>(M, f2_lin<2, 2>(S, 1, tx, -1)), 1, e8, -1));     // 6 x 4 -> (4, 6) + 2p - 8B^2
     f228 zl = f2_red(f2_scale(py, 2));                                                      // Z of 2P and P
     f228 rx = S, ry = e8;

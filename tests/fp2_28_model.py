@@ -285,3 +285,31 @@ def clear(P):
     t3 = jadd(t3, t2)
     t3 = jadd(t3, jneg(t1))
     return jadd(t3, jneg(P))
+
+
+def coz_table(px, py, ne):
+    """k_recover.hip k_wnaf_table_g2 on the model: the odd multiples P, 3P, ..., (2 ne - 1) P of an affine P by DBLU and
+    ZADDU co-Z steps, line by line as on the device. Returns the entries as Jacobian triples (entry 0 affine, Z = 1)
+    and the factors d_j (Z_j = Z_{j-1} d_j), so the walk back from 1 / Z_last can be checked too."""
+    B = red2(s2(py, 2))
+    S = red2(scale2(red2(m2(px, B)), 4))
+    Mv = scale2(red2(s2(px, 2)), 3)                                        # < 6
+    tx = red2(lin2(4, 4, s2(Mv, 6), 1, S, -2))
+    e8 = red2(scale2(red2(s2(B, 2)), 8))
+    ty = red2(lin2(2, 2, m2(Mv, lin2(2, 2, S, 1, tx, -1)), 1, e8, -1))
+    zl = red2(scale2(py, 2))
+    rx, ry = S, e8
+    entries, ds = [(px, py, ONE2)], []
+    for _ in range(1, ne):
+        d = lin2(2, 2, tx, 1, rx, -1)                                      # < 4
+        C = red2(s2(d, 4))
+        w1, w2 = red2(m2(tx, C)), red2(m2(rx, C))
+        ee = lin2(2, 2, ty, 1, ry, -1)                                     # < 4
+        a1 = red2(m2(ty, lin2(2, 2, w1, 1, w2, -1)))
+        rx = red2(lin32(4, 4, s2(ee, 4), 1, w1, -1, w2, -1))
+        ry = red2(lin2(2, 2, m2(ee, lin2(2, 2, w1, 1, rx, -1)), 1, a1, -1))
+        tx, ty = w1, a1
+        zl = red2(m2(zl, d))
+        ds.append(red2(d))
+        entries.append((rx, ry, zl))
+    return entries, ds

@@ -186,3 +186,21 @@ def test_unnormalised_product_operands():
     max_add = 2 * mask
     column = 14 * max_add * max_sub + 14 * mask * mask + (1 << 36)
     assert max_sub < 2 ** 29.6 and column < 2 ** 63
+
+
+def test_coz_odd_multiples_table():
+    """k_wnaf_table_g2's co-Z chain on the model (fp2_28_model.coz_table, every product and sum bound-checked): entry j
+    is (2j + 1) P for subgroup points, and 1 / Z_{j-1} = d_j / Z_j walks the last entry's inverse back over the table."""
+    rng = random.Random(21)
+    inv2 = lambda a: B.f2inv(a)  # noqa: E731
+    for _ in range(6):
+        pt = g2_point(rng)
+        px, py = enc(pt)
+        for ne in (4, 8):
+            entries, ds = M.coz_table(px, py, ne)
+            for j, (X, Y, Z) in enumerate(entries):
+                assert M.to_affine((X, Y, Z, False)) == B.ec_mul(B.FP2, pt, 2 * j + 1), (ne, j)
+            zi = inv2(M.to_f2(entries[-1][2]))
+            for j in range(ne - 1, 0, -1):
+                assert B.f2mul(zi, M.to_f2(entries[j][2])) == (1, 0)
+                zi = B.f2mul(zi, M.to_f2(ds[j - 1]))
