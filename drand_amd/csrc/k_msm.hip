@@ -953,6 +953,15 @@ hipError_t launch_msm_prep28(int sig_g2, size_t n, uint8_t* status, const uint32
   return hipGetLastError();
 }
 
+// Block size of the reduction kernels: 64 threads when the launch holds at most one wave per CU (level 0's few rows),
+// so its waves land on separate CUs instead of four to a CU. These kernels spill (G2: ~1 KB per lane) and run one wave
+// per SIMD, so their time is the latency of scratch round trips through the CU's vector cache, which four waves on one
+// CU share: the G2 level-0 row tree took 1.13 ms in 256-thread blocks and 0.58 ms in 64-thread blocks (rocprofv3
+// single-stream batches, profiles/r05/rocprof_unchained_rowtree_blk*_r05x2.csv). Launches with more waves keep
+// 256-thread blocks (the row tree's LDS buffer is sized for 256 lanes: one 64-lane block per CU would cap the many-row
+// launches at 256 waves).
+static unsigned few_waves_block(size_t nthreads) { return nthreads <= 256 * 64 ? 64u : 256u; }
+
 // nsets = 2: the sigma points S and the hash points Q share the sorted lists (the batch check); 1: S only
 template <class C>
 static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, const uint32_t* Q, msm_ws& ws, hipStream_t st,
@@ -976,10 +985,11 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     }
   }
   const size_t rows = ngroups * g.nwin, ngw = (size_t)nsets * rows;
-  hipLaunchKernelGGL(k_msm_segsum28<C>, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs,
+  const unsigned sb = few_waves_block(ngw * g.nseg);
+  hipLaunchKernelGGL(k_msm_segsum28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs,
                      ws.runs);
   if (g.nseg > 1)
-    hipLaunchKernelGGL(k_msm_segoff28<C>, dim3(nblk(ngw * g.nseg, 256)), dim3(256), 0, st, g, ngw, ws.segs, ws.runs);
+    hipLaunchKernelGGL(k_msm_segoff28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, g, ngw, ws.segs, ws.runs);
   // row sums: ws.runs (free after the offsets) when a row's lanes fit one wave; else the waves' partials go to ws.runs
   // and the row sums to ws.segs
   // G: 8 when the rows' segments are many (the additions' count matters: the bisection's and the tbls per-signer
@@ -995,8 +1005,8 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
   }
   const uint32_t* rowsum = ws.runs;
   if (g.nseg > 1)
-    hipLaunchKernelGGL(k_msm_rowtree28<C>, dim3(nblk(ngw * lpr, 256)), dim3(256), 0, st, ws.segs, g.nseg, G, ngw, lpr, span,
-                       ws.runs);
+    hipLaunchKernelGGL(k_msm_rowtree28<C>, dim3(nblk(ngw * lpr, few_waves_block(ngw * lpr))), dim3(few_waves_block(ngw * lpr)), 0,
+                       st, ws.segs, g.nseg, G, ngw, lpr, span, ws.runs);
   else
     rowsum = ws.segs;  // one segment per row: its value is the row sum
   if (lpr > 64) {
