@@ -13,6 +13,7 @@
 #   pmc:<counters>[@<args>] one rocprofv3 --pmc pass of bench.py <args> -> gpurun_out/pmc_<tag>_<i>/
 #   pmccfg:<counters>@<args> one rocprofv3 --pmc pass of bench/bench_configs.py <args> -> gpurun_out/pmc_<tag>_<i>/
 #   py:<script args>       python <script args>              -> gpurun_out/py_<tag>_<i>.log
+#   rocprofpy:<script args> rocprofv3 --kernel-trace --stats of python3 <script args> -> gpurun_out/prof_<tag>_<i>/
 #   env:<NAME>=<value>     export a variable for the steps after it (env:NAME= clears it)
 #   sh:<script args>       bash <script args> (bench/pmc.sh, bench/bisect_sweep.sh: they time-limit their own steps)
 set -euo pipefail
@@ -69,6 +70,10 @@ for step in "$@"; do
     py)
       timeout -k 10 600 python $arg > "$O/py_${T}_$i.log" 2>&1
       tail -5 "$O/py_${T}_$i.log" ;;
+    rocprofpy)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_${T}_$i" -o run -- python3 $arg \
+        > "$O/prof_${T}_$i.log" 2>&1
+      tail -3 "$O/prof_${T}_$i.log" ;;
     env)
       export "$arg" ;;
     sh)

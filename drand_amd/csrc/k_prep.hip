@@ -82,6 +82,71 @@ __global__ __launch_bounds__(256, 2) void k_sub_sig_g2(size_t n, uint8_t* __rest
   }
 }
 
+// ---------------------------------------------------------------- small-batch path (drandhip.cpp verify_small)
+// The signature pass split at the decoded point: the per-round pairing check needs only the point, so it starts as soon
+// as the decode finishes and runs beside the subgroup test, whose result is ANDed into the verdict at the end
+// (k_and_subgroup). A G1 round's decode is a fraction of k_prep_sig<fp> (one square root); the test (two [|u|] chains)
+// is the rest. The subgroup kernels write only sub_bad (the point and status stay as the pairing check reads them).
+__global__ __launch_bounds__(64) void k_dec_sig_g1(const uint8_t* __restrict__ sigs, size_t stride, size_t n,
+                                                   uint8_t* __restrict__ status, uint32_t* __restrict__ sig_aff,
+                                                   uint8_t* __restrict__ rand_out) {
+  size_t i = gtid();
+  if (i >= n) return;
+  const uint8_t* s = sigs + i * stride;
+  aff<fp> a;
+  uint8_t st = g1_decompress(a, s, false);
+  if (rand_out) st_digest(rand_out + 32 * i, sha256_aligned<48>(s));
+  if (st != DEC_OK) {
+    a.x = fp{};
+    a.y = fp{};
+    st = DEC_BAD;  // infinity signatures are rejected like kilic's engine + kyber's verify
+  }
+  status[i] = st;
+  st_aff_aos<fp>(sig_aff, i, a);
+}
+
+template <class F>
+__global__ __launch_bounds__(64) void k_sub_flag(size_t n, const uint8_t* __restrict__ status, const uint32_t* __restrict__ sig_aff,
+                                                 uint8_t* __restrict__ sub_bad) {
+  size_t i = gtid();
+  if (i >= n) return;
+  bool bad = false;
+  if (status[i] == DEC_OK) {
+    if constexpr (sizeof(F) == sizeof(fp)) bad = !g1_in_subgroup28([&] { return ld_aff_aos<fp>(sig_aff, i); });
+    else bad = !g2_in_subgroup28([&] { return ld_aff_aos<fp2>(sig_aff, i); });
+  }
+  sub_bad[i] = bad ? 1 : 0;
+}
+
+__global__ __launch_bounds__(64) void k_and_subgroup(size_t n, const uint8_t* __restrict__ sub_bad, uint8_t* __restrict__ verdict) {
+  size_t i = gtid();
+  if (i >= n) return;
+  if (sub_bad[i]) verdict[i] = 0;
+}
+
+hipError_t launch_dec_sig(int sig_g2, const uint8_t* sigs, size_t stride, size_t n, uint8_t* status, uint32_t* sig_aff,
+                          uint8_t* rand_out, hipStream_t st) {
+  if (!n) return hipSuccess;
+  if (sig_g2)
+    hipLaunchKernelGGL(k_dec_sig_g2, dim3(nblk(n, 256)), dim3(256), 0, st, sigs, stride, n, status, sig_aff, rand_out);
+  else
+    hipLaunchKernelGGL(k_dec_sig_g1, dim3(nblk(n, 64)), dim3(64), 0, st, sigs, stride, n, status, sig_aff, rand_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sub_flag(int sig_g2, size_t n, const uint8_t* status, const uint32_t* sig_aff, uint8_t* sub_bad, hipStream_t st) {
+  if (!n) return hipSuccess;
+  if (sig_g2) hipLaunchKernelGGL(k_sub_flag<fp2>, dim3(nblk(n, 64)), dim3(64), 0, st, n, status, sig_aff, sub_bad);
+  else hipLaunchKernelGGL(k_sub_flag<fp>, dim3(nblk(n, 64)), dim3(64), 0, st, n, status, sig_aff, sub_bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_and_subgroup(size_t n, const uint8_t* sub_bad, uint8_t* verdict, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_and_subgroup, dim3(nblk(n, 64)), dim3(64), 0, st, n, sub_bad, verdict);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- prep: messages -> hash points (no cofactor)
 // G1 (fused): hash_to_curve without clear_cofactor, one round per lane
 __global__ __launch_bounds__(256, occ<fp>::W) void k_prep_msg_g1(const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs,

@@ -64,6 +64,12 @@ inline size_t msm_meta_bytes(size_t max_entries) { return msm_nchunks(max_entrie
 
 hipError_t launch_prep(int sig_g2, const uint8_t* sigs, size_t stride, size_t n, uint8_t* status, uint32_t* sig_aff,
                        uint8_t* rand_out, hipStream_t st);
+// small-batch path: the signature pass split at the decoded point (decode + randomness; subgroup test -> sub_bad[i]
+// = 1 when a decoded point is not in the subgroup; verdict[i] = 0 where sub_bad[i])
+hipError_t launch_dec_sig(int sig_g2, const uint8_t* sigs, size_t stride, size_t n, uint8_t* status, uint32_t* sig_aff,
+                          uint8_t* rand_out, hipStream_t st);
+hipError_t launch_sub_flag(int sig_g2, size_t n, const uint8_t* status, const uint32_t* sig_aff, uint8_t* sub_bad, hipStream_t st);
+hipError_t launch_and_subgroup(size_t n, const uint8_t* sub_bad, uint8_t* verdict, hipStream_t st);
 // hash points Q_i (before cofactor clearing) of the beacon digests of (rounds, prevs) or of the given 32-byte
 // msgs32; a chained record longer than its slot marks status[i] = DEC_BAD. tmp: hash_tmp_bytes(sig_g2, n).
 size_t hash_tmp_bytes(int sig_g2, size_t n);
@@ -122,6 +128,11 @@ hipError_t launch_group_check_vm_c(const uint32_t* A, const uint32_t* B, size_t 
 hipError_t launch_leaf_check_vm(int sig_g2, const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
                                 const uint32_t* key_aff, const uint32_t* key_h, const uint8_t* status, uint32_t* pairs,
                                 uint8_t* live, uint8_t* done, uint8_t* verdict, hipStream_t st);
+
+// G2-signature leaves with the hash point's clearing inside the program (NP2C); same buffers as launch_group_check_vm_c
+hipError_t launch_leaf_check_vm_c(const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
+                                  const uint32_t* key_aff, const uint8_t* status, uint32_t* pairs, uint8_t* live, uint8_t* done,
+                                  uint8_t* verdict, hipStream_t st);
 
 hipError_t launch_multi_pairing_vm(const uint32_t* P, const uint32_t* Q, size_t n, uint32_t* pairs, uint8_t* live,
                                    uint32_t* f_tmp, uint8_t* pass, hipStream_t st);
