@@ -29,6 +29,7 @@ bounded sample, on the host cores this process may use. "single_call": one dh_ve
 import argparse
 import collections
 import ctypes
+import datetime
 import hashlib
 import json
 import os
@@ -69,6 +70,8 @@ def parse():
     ap.add_argument("--single-call-steps", type=int, default=4, help="one-call-at-a-time batches timed after")
     ap.add_argument("--single-call-split", default="0,1", help="chunk rounds,workers of the one-call split (library "
                     "default: none)")
+    ap.add_argument("--single-beacon-reps", type=int, default=20,
+                    help="one-beacon latency calls per scheme (bench/single_beacon.py); 0: skip")
     ap.add_argument("--streams", type=int, default=8,
                     help="batches in flight per GPU (local check: host threads, each with its own library worker; "
                          "node-wide check: one host thread keeping this many batches queued)")
@@ -79,6 +82,12 @@ def parse():
                     help="node-wide RLC check with an all-gather of partial sums (auto: when N > 1)")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="GPU_MAX_HW_QUEUES for this process (0: keep the environment's)")
+    ap.add_argument("--collective-timeout", type=float, default=300.0,
+                    help="process-group timeout in seconds (init_process_group(timeout=...)): a collective blocked "
+                         "longer than this fails instead of hanging")
+    ap.add_argument("--batch-deadline", type=float, default=120.0,
+                    help="N > 1: seconds a node batch may stay unfinished before its rank reports the stall (rank, "
+                         "batch) and exits with status 3 (dist.BatchWatchdog); 0: off")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: rehearse N ranks on one GPU with host-staged collectives")
     ap.add_argument("--exchange", choices=["auto", "always"], default="auto",
@@ -170,7 +179,7 @@ def main():
     import torch
     import torch.distributed as dist
     from drand_amd import _lib, scheme_from_name
-    from drand_amd.dist import begin_node_batch, gather_verdicts, pack_bits, shard_rounds, strong_shard
+    from drand_amd.dist import BatchWatchdog, begin_node_batch, gather_verdicts, pack_bits, shard_rounds, strong_shard
 
     gloo = args.backend == "gloo"
     dev_index = 0 if gloo else local  # gloo rehearsal: every rank on GPU 0
@@ -188,10 +197,11 @@ def main():
             so.bind(("127.0.0.1", 0))
             os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(so.getsockname()[1])
             so.close()
+        tmo = datetime.timedelta(seconds=args.collective_timeout)
         if gloo:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=tmo)
         else:
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, timeout=tmo)
     node_check = args.node_check == "on" or (args.node_check == "auto" and world > 1)
 
     sch = scheme_from_name(args.scheme)
@@ -251,7 +261,8 @@ def main():
     rounds, sigs, t_sign = work.rounds, work.sigs, work.sign_s
     d_rounds, d_sigs = work.d_rounds, work.d_sigs
     torch.cuda.synchronize()
-    state = {"node_check": node_check}
+    state = {"node_check": node_check,
+             "watchdog": BatchWatchdog(args.batch_deadline, rank) if pg and args.batch_deadline > 0 else None}
 
     def verify(wk, slot):
         rc = lib.dh_verify_batch_device(sch.id, pk, len(pk), ctypes.c_void_p(wk.d_rounds.data_ptr()),
@@ -268,11 +279,16 @@ def main():
         pending = collections.deque()
         bits = []
         ht = state.setdefault("node_host_s", collections.Counter())
+        # a batch whose collective or check never completes (a dead or hung peer) ends this rank with a message naming
+        # the rank and the batch instead of a silent hang (dist.BatchWatchdog)
+        wd = state.get("watchdog")
 
         def retire():
-            slot, h = pending.popleft()
+            slot, h, key = pending.popleft()
             t0 = time.perf_counter()
             h.finish()
+            if wd is not None:
+                wd.end(key)
             t1 = time.perf_counter()
             bits.append(wk.pack(slot))
             ht["finish_wait"] += t1 - t0
@@ -288,9 +304,12 @@ def main():
             # ordered them all through torch's current stream and chained every batch's per-round kernels behind the
             # previous batch's MSM: 14.2 M/s at 131k rounds, 8 slots)
             t0 = time.perf_counter()
+            state["batch_seq"] = key = state.get("batch_seq", 0) + 1
+            if wd is not None:
+                wd.begin(key, "%d rounds, slot %d" % (wk.n, slot))
             pending.append((slot, begin_node_batch(lib, sch, pk, wk.d_rounds, wk.d_sigs, wk.n, wk.d_verdict[slot],
                                                    wk.d_rand[slot], wk.d_part[slot], world, None, stage_host=gloo,
-                                                   rank=rank, inputs_ready=True, exchange=xchg)))
+                                                   rank=rank, inputs_ready=True, exchange=xchg), key))
             ht["begin_exchange_check"] += time.perf_counter() - t0
         while pending:
             retire()
@@ -375,8 +394,8 @@ def main():
         strong = {"scaling": "strong", "rounds_total": args.strong_total_rounds, "rounds_per_gpu": swork.n,
                   "steps": args.steps, "value": round(args.strong_total_rounds * args.steps / s_el, 1),
                   "unit": "beacons/s", "ms_per_step": round(s_el * 1000.0 / args.steps, 3), "verdicts_ok": s_ok,
-                  "what": "one %d-round quicknet chain split over the %d ranks per step (node-wide RLC check), max-over-"
-                          "ranks wall time of the steps" % (args.strong_total_rounds, world)}
+                  "what": "one %d-round %s chain split over the %d ranks per step (node-wide RLC check), max-over-"
+                          "ranks wall time of the steps" % (args.strong_total_rounds, sch.name, world)}
         del swork
 
     # Roofline pass (after the timed region, not counted in `value`): with S batches in flight the kernels of
@@ -427,12 +446,29 @@ def main():
         del d_r4, d_s4, d_v4
         lib.dh_set_split(0, 1)
 
+    # the drop-in's one-beacon calls (VerifyBeacon / VerifyRecovered / one-round Recover), one at a time from the host,
+    # every scheme, warm and cold key cache, beside the CPU restatement's per-verify time on one core
+    # (bench/single_beacon.py; the small-batch path of drandhip.cpp verify_small)
+    single_beacon = None
+    if world == 1 and args.single_beacon_reps > 0:
+        sys.path.insert(0, os.path.join(ROOT, "bench"))
+        import single_beacon as sbm
+        sb = sbm.measure(reps=args.single_beacon_reps, with_oracle=not args.no_cpu_baseline)
+        ok = ok and all(v["verdicts_ok"] for v in sb.values())
+        single_beacon = {name: {k: (v["p50"] if isinstance(v, dict) else v) for k, v in e.items()
+                                if k not in ("recover_shape", "verdicts_ok")} for name, e in sb.items()}
+        single_beacon["what"] = ("p50 ms of one host call at a time (%d calls; cold = key-cache miss on every call; "
+                                 "recover = n 64 / t 33, one round); oracle = the C restatement on one core"
+                                 % args.single_beacon_reps)
+
     if pg:
         t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device="cpu" if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, bad = float(t[0]), float(t[1])
         ok = bad == 0.0
     if rank != 0:
+        if state["watchdog"] is not None:
+            state["watchdog"].stop()
         dist.destroy_process_group()
         return
 
@@ -485,6 +521,7 @@ def main():
         "stages_ms_per_step": {k: round(v["total_ms"] / args.steps, 3) for k, v in prof.items()},
         "stages_ms_single_stream": {k: round(v["total_ms"] / max(1, v["count"]), 3) for k, v in prof1.items()},
         "single_call": single,
+        "single_beacon_ms": single_beacon,
         "strong_scaling": strong,
         "node_host_ms_per_batch": ({k: round(v * 1000 / node_host["batches"], 3) for k, v in node_host.items()
                                     if k != "batches"} if node_host.get("batches") else None),
@@ -493,6 +530,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sch.name, pk, rounds, sigs, args.cpu_sample_seconds)
     print(json.dumps(out), flush=True)
+    if state["watchdog"] is not None:
+        state["watchdog"].stop()
     if pg:
         dist.destroy_process_group()
 

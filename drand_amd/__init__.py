@@ -7,6 +7,8 @@ over that ABI; see drand_amd.scheme.
 from .scheme import (  # noqa: F401
     Scheme,
     SchemeError,
+    DeviceError,
+    DeviceBusy,
     scheme_from_name,
     list_schemes,
     DEFAULT_SCHEME,

@@ -1351,7 +1351,9 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
                                       w->r_own.as<uint32_t>(), g2 ? 0 : 1, st);
   }));
   // tables of 8 odd multiples when some round has a Lagrange basis of its own (its wave then runs the regular windows
-  // in k_lagrange), else of 4 for the width-4 NAF: one word back from the device
+  // in k_lagrange), else of 4 for the width-4 NAF: one word back from the device. k_lagrange depends on this: k_lambda
+  // writes width-4 NAF nibbles for round 0's basis only, so entries == 4 is valid only when every round uses basis 0
+  // (own == 0); k_lagrange leaves a wave at infinity (not recovered) if that ever fails to hold
   int entries = 4;
   if (g2) {
     uint32_t own = 0;

@@ -1001,7 +1001,9 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     for (span = 1; span < lpr;) span *= 2;
     lpr = span;
   } else if (lpr % 64) {
-    return hipErrorInvalidValue;  // fit_segments: rows of more than 512 segments hold a multiple of 512
+    // whole waves per row (fit_segments keeps rows of more than 512 segments at a multiple of 512, but the recover and
+    // tbls callers do not run it): the extra lanes start past nseg and add the identity
+    lpr = (lpr + 63) / 64 * 64;
   }
   const uint32_t* rowsum = ws.runs;
   if (g.nseg > 1)

@@ -534,7 +534,13 @@ __global__ __launch_bounds__(64 * LG_LANES) void k_lagrange(const uint32_t* __re
   // (a wave coherent on a basis other than round 0's runs the regular windows too: k_lambda writes the width-4 NAF
   // nibbles for round 0's basis only)
   const bool regular = reg && (!__all(!live || myset == ref) || ref != 0);
-  if (live) {
+  // G2: the width-4 NAF nibbles exist for round 0's basis only (k_lambda parks x_m in the other bases' nibble words),
+  // so a wave on another basis needs the regular windows, i.e. tables of 8 entries (reg). The host sets reg whenever
+  // any round has a basis of its own (drandhip.cpp recover_core, `own`), so this never fires; if it did, the wave's
+  // rounds are left at infinity, which VerifyRecovered rejects (not recovered) instead of reading x_m values as digits.
+  // (G1 chains read NAF digit masks, which k_lambda writes for every basis.)
+  const bool lost_basis = sizeof(F) == sizeof(fp2) && !reg && ref != 0;
+  if (live && !lost_basis) {
     const uint32_t* L = lam + (lam_set ? (size_t)lam_set[j] : j) * t * LAM_WORDS;  // per term: NAF masks, wNAF nibbles
     const uint32_t* Sel = sel + j * (size_t)t;
     const int nt = q < t ? (t - q + nl - 1) / nl : 0;  // terms of this lane: k = q + nl i

@@ -15,6 +15,11 @@
   batch together instead of blocking in the collective. No data-path collective besides that (the per-round data
   never leaves its GPU).
 * Verdicts: packed bitmaps all-gathered once at the end (gather_verdicts).
+* Stalls: a rank whose peer died or hangs would wait in the collective (or in the batch's host wait behind it) for
+  ever. BatchWatchdog gives every in-flight node batch a deadline: past it the rank names itself, the batch and how
+  long it has waited on stderr and exits with STALL_EXIT (a child process exit, never an exec), so the launcher tears
+  the job down instead of hanging; the process group's own collective timeout (init_process_group(timeout=...)) is the
+  second line behind it.
 * replay_shard: the sharded CheckPastBeacons (chain/beacon/sync_manager.go:170-235) built from the pieces above;
   recover_shard: tbls Recover with its rounds sharded (no exchange before the gather).
 The collectives use torch.distributed: backend "nccl" (= RCCL) with device tensors, "gloo" with host tensors
@@ -22,6 +27,10 @@ The collectives use torch.distributed: backend "nccl" (= RCCL) with device tenso
 """
 import ctypes
 import hashlib
+import os
+import sys
+import threading
+import time
 
 import numpy as np
 
@@ -195,6 +204,65 @@ class _nullcontext:
 
     def __exit__(self, *a):
         return False
+
+
+STALL_EXIT = 3
+
+
+class BatchWatchdog:
+    """Deadline per in-flight node batch. begin(key, what) when a batch is begun, end(key) when its finish() returned;
+    a daemon thread checks the oldest in-flight batch every `poll` seconds, and once it is older than `deadline`
+    seconds reports "rank R: node batch K stalled ..." on stderr and calls on_stall(message) — by default
+    os._exit(STALL_EXIT): the thread that would report is blocked in a collective or in the library's host wait (ctypes
+    and the collectives release the GIL), so raising in it is not possible. A deadline <= 0 disables the watchdog."""
+
+    def __init__(self, deadline, rank, on_stall=None, poll=None):
+        self.deadline, self.rank = float(deadline), rank
+        self.on_stall = on_stall or self._exit
+        self.poll = poll if poll is not None else max(0.05, min(1.0, self.deadline / 8))
+        self._live = {}
+        self._mu = threading.Lock()
+        self._stop = threading.Event()
+        self.fired = None
+        self._th = None
+        if self.deadline > 0:
+            self._th = threading.Thread(target=self._run, name="node-batch-watchdog", daemon=True)
+            self._th.start()
+
+    @staticmethod
+    def _exit(msg):
+        sys.stderr.flush()
+        os._exit(STALL_EXIT)
+
+    def begin(self, key, what=""):
+        with self._mu:
+            self._live[key] = (time.monotonic(), what)
+
+    def end(self, key):
+        with self._mu:
+            self._live.pop(key, None)
+
+    def stop(self):
+        self._stop.set()
+        if self._th is not None:
+            self._th.join(timeout=5)
+
+    def _run(self):
+        while not self._stop.wait(self.poll):
+            with self._mu:
+                old = min(self._live.items(), key=lambda kv: kv[1][0]) if self._live else None
+            if old is None:
+                continue
+            key, (t0, what) = old
+            waited = time.monotonic() - t0
+            if waited > self.deadline:
+                msg = ("rank %d: node batch %s stalled: not finished %.1f s after it began (deadline %.1f s; %s) -- its "
+                       "all-gather or node check never completed, a peer rank has likely died or hangs; exiting with "
+                       "status %d" % (self.rank, key, waited, self.deadline, what or "node-wide check", STALL_EXIT))
+                print(msg, file=sys.stderr, flush=True)
+                self.fired = msg
+                self.on_stall(msg)
+                return
 
 
 def _status_offset(pb):

@@ -37,12 +37,20 @@ class DeviceError(RuntimeError):
     """libdrandhip reported a device / runtime failure."""
 
 
+class DeviceBusy(DeviceError):
+    """DH_EBUSY: every library worker is held by unfinished node batches (dh_batch_begin without dh_batch_finish)
+    for longer than DRANDHIP_LEASE_TIMEOUT_MS. Nothing was verified; the call may be retried once the node batches
+    have been finished (a thread that holds them must finish them first, or it waits on itself)."""
+
+
 def _check(rc):
     if rc >= 0:
         return rc
     msg = _lib.last_error()
     if rc in (_lib.DH_EINVAL, _lib.DH_EKEY, _lib.DH_ERECOVER):
         raise SchemeError(msg)
+    if rc == _lib.DH_EBUSY:
+        raise DeviceBusy("libdrandhip error %d (busy): %s" % (rc, msg))
     raise DeviceError("libdrandhip error %d: %s" % (rc, msg))
 
 

@@ -211,6 +211,85 @@ def test_node_batch_protocol_gloo(fail_rank):
     assert rank_seed(0, 3) == 0
 
 
+class _StallLib(_FakeLib):
+    """rank `stall_rank`'s dh_batch_begin never returns in time (a hung peer): it sleeps for `secs`"""
+
+    def __init__(self, rank, stall_rank, pb, secs):
+        super().__init__(rank, None, pb)
+        self.stall_rank, self.secs = stall_rank, secs
+
+    def dh_batch_begin(self, *a):
+        import time
+        if self.rank == self.stall_rank:
+            time.sleep(self.secs)
+        return super().dh_batch_begin(*a)
+
+
+def _stall_worker(rank, world, port, out_dir):
+    import datetime
+    from drand_amd.dist import BatchWatchdog, STALL_EXIT
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    # the process group's own timeout is the second line: longer than the watchdog's deadline
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    from drand_amd.scheme import scheme_from_name
+    s = scheme_from_name("pedersen-bls-unchained")
+    pb = 2 * 72 * 4 + 16
+    lib = _StallLib(rank, 1, pb, 600)
+
+    def on_stall(msg):
+        with open(os.path.join(out_dir, "stall_%d.txt" % rank), "w") as f:
+            f.write(msg)
+        os._exit(STALL_EXIT)
+
+    wd = BatchWatchdog(2.0, rank, on_stall=on_stall, poll=0.2)
+    for k in range(3):
+        wd.begin(k, "test batch")
+        verify_node_batch(lib, s, b"k" * 48, None, None, 10, None, None, torch.zeros(pb, dtype=torch.uint8), world, seed=5)
+        wd.end(k)
+    os._exit(0)
+
+
+def test_node_batch_stall_exits_with_message(tmp_path):
+    """a rank whose peer hangs (rank 1 never returns from dh_batch_begin) must not wait in the
+    all-gather for ever. Every rank's BatchWatchdog names the rank and the stalled batch and the rank exits with
+    STALL_EXIT (3): rank 0 from inside the blocked all-gather, rank 1 from inside its stalled begin."""
+    from drand_amd.dist import STALL_EXIT
+    world = 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_stall_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=90)
+        if p.exitcode is None:
+            p.kill()
+    assert [p.exitcode for p in procs] == [STALL_EXIT, STALL_EXIT]
+    for r in range(world):
+        msg = open(os.path.join(str(tmp_path), "stall_%d.txt" % r)).read()
+        assert msg.startswith("rank %d: node batch 0 stalled" % r), msg
+
+
+def test_watchdog_quiet_when_batches_finish():
+    from drand_amd.dist import BatchWatchdog
+    fired = []
+    wd = BatchWatchdog(0.5, 0, on_stall=fired.append, poll=0.05)
+    import time
+    for k in range(5):
+        wd.begin(k)
+        time.sleep(0.05)
+        wd.end(k)
+    time.sleep(0.8)
+    wd.stop()
+    assert fired == [] and wd.fired is None
+    wd = BatchWatchdog(0.3, 4, on_stall=fired.append, poll=0.05)
+    wd.begin("b7")
+    time.sleep(1.0)
+    wd.stop()
+    assert len(fired) == 1 and fired[0].startswith("rank 4: node batch b7 stalled")
+
+
 # ---------------------------------------------------------------- sharded tbls Recover (config 4 over the node)
 class _OracleRecoverScheme:
     """Stands in for drand_amd.scheme.Scheme.recover_batch on the CPU: the oracle's per-round Recover (kyber sign/tbls

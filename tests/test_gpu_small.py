@@ -250,3 +250,49 @@ def test_np2c_group_check_branches(dh):
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
     assert json.loads(p.stdout.strip().splitlines()[-1]) == got
+
+
+# ---------------------------------------------------------------- DH_EBUSY from a blocking call
+_BUSY_CHILD = r"""
+import ctypes, sys
+sys.path.insert(0, %(root)r)
+import numpy as np, torch
+torch.zeros(1, device="cuda")
+import drand_amd
+from drand_amd import _lib
+lib = _lib.load()
+assert lib.dh_init(0) == 0
+s = drand_amd.scheme_from_name("bls-unchained-g1-rfc9380")
+sk = bytes(31) + b"\x05"
+pk = s.public_key(sk)
+rounds = np.arange(1, 101, dtype=np.uint64)
+sigs = s.sign_beacons(sk, rounds)
+d_r = torch.from_numpy(rounds.view(np.int64)).cuda()
+d_s = torch.from_numpy(sigs).cuda()
+d_v = torch.zeros(100, dtype=torch.uint8, device="cuda")
+part = torch.zeros(lib.dh_partial_bytes(s.id), dtype=torch.uint8, device="cuda")
+torch.cuda.synchronize()
+b = ctypes.c_void_p()
+ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+assert lib.dh_batch_begin(s.id, pk, len(pk), ptr(d_r), ptr(d_s), 48, None, 0, None, 100, ptr(d_v), None, 1, None,
+                          ctypes.byref(b), ptr(part)) == 0, _lib.last_error()
+# the only worker is held by the node batch: a blocking call waits DRANDHIP_LEASE_TIMEOUT_MS, then DH_EBUSY
+try:
+    s.verify_beacons(pk, rounds[:3], sigs[:3])
+    print("NOT-BUSY")
+except drand_amd.DeviceBusy as e:
+    print("BUSY", e)
+assert lib.dh_batch_finish(b, 1, None) >= 0, _lib.last_error()
+v, _ = s.verify_beacons(pk, rounds[:3], sigs[:3])
+print("AFTER", bool(v.all()))
+"""
+
+
+def test_blocking_call_busy_then_succeeds():
+    env = dict(os.environ, DRANDHIP_MAX_WORKERS="1", DRANDHIP_LEASE_TIMEOUT_MS="200")
+    p = subprocess.run([sys.executable, "-c", _BUSY_CHILD % {"root": ROOT}], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    out = p.stdout.split("\n")
+    assert any(line.startswith("BUSY libdrandhip error -6") for line in out), p.stdout
+    assert "AFTER True" in out, p.stdout
