@@ -457,7 +457,7 @@ def main():
         ok = ok and all(v["verdicts_ok"] for v in sb.values())
         single_beacon = {name: {k: (v["p50"] if isinstance(v, dict) else v) for k, v in e.items()
                                 if k not in ("recover_shape", "verdicts_ok")} for name, e in sb.items()}
-        single_beacon["what"] = ("p50 ms of one host call at a time (%d calls; cold = key-cache miss on every call; "
+        single_beacon["what"] = ("p50 ms of one host call at a time (%d calls; cold = key-cache miss on every call (6 keys cycled), two_keys = two keys alternating; "
                                  "recover = n 64 / t 33, one round); oracle = the C restatement on one core"
                                  % args.single_beacon_reps)
 

@@ -16,8 +16,8 @@ O=$R/gpurun_out
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$TAG" -o run --output-format csv -- \
-  python3 "$R/bench.py" --steps 8 --warmup 8 --single-call-steps 0 --no-cpu-baseline > "$O/prof_$TAG.log" 2>&1
-SMALL="--total-rounds 262144 --steps 1 --warmup 0 --streams 1 --roofline-steps 0 --single-call-steps 0 --no-cpu-baseline"
+  python3 "$R/bench.py" --steps 8 --warmup 8 --single-call-steps 0 --single-beacon-reps 0 --no-cpu-baseline > "$O/prof_$TAG.log" 2>&1
+SMALL="--total-rounds 262144 --steps 1 --warmup 0 --streams 1 --roofline-steps 0 --single-call-steps 0 --single-beacon-reps 0 --no-cpu-baseline"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$O/pmc_fetch_$TAG" -o pmc --output-format csv -- python3 "$R/bench.py" $SMALL \
   > "$O/pmc_fetch_$TAG.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$O/pmc_write_$TAG" -o pmc --output-format csv -- python3 "$R/bench.py" $SMALL \

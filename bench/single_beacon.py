@@ -3,7 +3,8 @@
 beacon — VerifyBeacon (gossip validator lp2p/client/validator.go:62, client/verify.go:192), VerifyRecovered
 (chain/beacon/chainstore.go:207) and a one-round Recover (the aggregator, chainstore.go:202) — timed one at a time
 from the host, per scheme, with the group key cached on the worker ("warm") and with a key-cache miss on every call
-("cold": two keys alternate). Beside them, the CPU oracle's per-verify time on one core (context only: a C
+("cold": six keys cycled, more than a worker's 4-slot key cache holds; "two_keys": two chains' keys alternating,
+both cached). Beside them, the CPU oracle's per-verify time on one core (context only: a C
 restatement, not kyber).
 
     python bench/single_beacon.py [--reps 40] [--out gpurun_out/single_beacon.json]
@@ -66,6 +67,9 @@ def measure(schemes=SCHEMES, reps=40, recover_nt=(64, 33), with_oracle=True):
         s = scheme_from_name(name)
         sk1, sk2 = _sk(b"single-1-" + name.encode()), _sk(b"single-2-" + name.encode())
         pk1, pk2 = s.public_key(sk1), s.public_key(sk2)
+        # cold: more keys than a worker's key cache holds (drandhip.cpp KEY_SLOTS = 4), cycled, so every call misses
+        cold_keys = [(s.public_key(_sk(b"single-c%d-" % c + name.encode())), _sk(b"single-c%d-" % c + name.encode()))
+                     for c in range(6)]
         rounds = np.arange(1000, 1000 + reps + 1, dtype=np.uint64)
         prevs = None
         if s.chained:
@@ -88,11 +92,19 @@ def measure(schemes=SCHEMES, reps=40, recover_nt=(64, 33), with_oracle=True):
         bad[20] ^= 1
         ok &= lib.dh_verify_beacon(s.id, pk1, len(pk1), int(rounds[1]), bytes(bad), s.sig_len, prev_b[1], len(prev_b[1])) == 0
         ok &= vb(pk1, sig1, 2) == 1 and vb(pk2, sig1, 2) == 0  # a key switch (cold) rejects the other key's signature
-        cold_t = []
+        two_t = []  # two keys alternating (a node serving two chains): both stay cached
         for k in range(max(6, reps // 4)):
             pk, sg = (pk2, sig2) if k % 2 == 0 else (pk1, sig1)
             t0 = time.perf_counter()
             r = vb(pk, sg, k % len(rounds))
+            two_t.append(time.perf_counter() - t0)
+            ok &= r == 1
+        cold_sigs = [s.sign_beacons(csk, rounds[:1], prevs[:1] if prevs is not None else None) for _, csk in cold_keys]
+        cold_t = []
+        for k in range(12):
+            cpk, _ = cold_keys[k % len(cold_keys)]
+            t0 = time.perf_counter()
+            r = vb(cpk, cold_sigs[k % len(cold_keys)], 0)
             cold_t.append(time.perf_counter() - t0)
             ok &= r == 1
         vb(pk1, sig1, 0)
@@ -106,6 +118,7 @@ def measure(schemes=SCHEMES, reps=40, recover_nt=(64, 33), with_oracle=True):
         rec_v = _time(lambda: vr(next(k_it2) % len(rounds)), reps)
         ok &= vr(3) == 1
         entry = {"verify_beacon_warm": _stats(warm), "verify_beacon_cold": _stats(cold_t),
+                 "verify_beacon_two_keys": _stats(two_t),
                  "verify_recovered_warm": _stats(rec_v)}
         # one-round Recover as the aggregator makes it: n signers, threshold t, the first t partials of the round
         n, t = recover_nt

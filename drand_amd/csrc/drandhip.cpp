@@ -125,17 +125,27 @@ struct worker {
   std::vector<uint8_t> h_verdict;
   // Recover: the (scheme, t, n_nodes, commits) whose decoded commits and public shares r_caff / r_shares hold
   std::vector<uint8_t> r_pub_key;
-  // decoded group key cache: the same key is used for every batch of a chain
-  uint8_t cached_key[96];
-  size_t cached_key_len = 0;
-  int cached_key_g2 = -1;
-  uint8_t cached_key_ok = 0;
+  // decoded group keys, KEY_SLOTS per worker (least recently used replaced): a chain's batches all use one key, and a
+  // node or relay serving several chains alternates between a few; key_cur = the slot ensure_key selected (96 words:
+  // the affine point, then [h_eff] pk for G1-signature schemes)
+  static constexpr int KEY_SLOTS = 4;
+  struct key_slot {
+    uint8_t bytes[96];
+    size_t len = 0;  // 0: empty
+    int g2 = -1;
+    uint8_t ok = 0;
+    uint64_t used = 0;
+  } keys[KEY_SLOTS];
+  uint64_t key_clock = 0;
+  dbuf key_tab;
+  uint32_t* key_cur = nullptr;
   // fault density (faults per round) the last bisection of this worker observed at its first level: a replay's
   // consecutive windows fail alike, so a dense one starts its next bisection with smaller groups (next_group_size)
   double fault_density = 0;
   // set by dh_batch_begin while it queues a node batch on one stream (node_one_stream): no tail-stream handoff
   bool begin_one_stream = false;
   void release_all() {
+    key_tab.release();
     dbuf* all[] = {&s28, &q28, &entries_alt, &cflags, &crank, &cscan, &status, &sig_aff, &q_pts, &scal, &entries, &verdict_tmp, &rand_tmp, &h2c_tmp, &in_rounds, &in_sigs,
                    &in_prevs, &in_prev_lens, &out_verdict, &out_rand, &key_raw, &key_aff, &key_ok, &cnt, &off,
                    &scan_tmp, &list, &buckets, &segs, &outA, &outB, &out2, &pass, &part, &meta, &vm_pairs, &vm_live, &vm_done, &r_commits, &r_cstatus, &r_caff, &r_shares,
@@ -290,27 +300,39 @@ int set_device_and_stream(worker* w, bool need_tail = true) {
   return DH_OK;
 }
 
-// The group key decoded on the device (key_aff: the affine point, then [h_eff] pk for G1-signature schemes), cached
-// per worker: a chain's batches all use one key, and decoding a G2 key is a ~9.5 ms one-lane kernel. On a miss the
-// stream is synchronised once to read the key's status; DH_EKEY when it is not a compressed subgroup point.
+// The group key decoded on the device (a key_tab slot: the affine point, then [h_eff] pk for G1-signature schemes),
+// cached per worker in KEY_SLOTS slots: a chain's batches all use one key, and decoding a G2 key is a one-lane kernel
+// of a few ms. On a miss the stream is synchronised once to read the key's status; DH_EKEY when it is not a
+// compressed subgroup point. Sets w->key_cur.
 int ensure_key(worker* w, bool g2, const uint8_t* pk, size_t pk_len, hipStream_t st) {
   HIP_TRY(w->key_raw.ensure(96));
-  HIP_TRY(w->key_aff.ensure(96 * 4));  // fixed size keeps the cache valid
-  HIP_TRY(w->key_ok.ensure(64));       // [0] key status, [32..63] RLC seed
-  const bool hit = w->cached_key_len == pk_len && w->cached_key_g2 == (g2 ? 0 : 1) && !memcmp(w->cached_key, pk, pk_len);
-  if (!hit) {
-    w->cached_key_len = 0;
+  HIP_TRY(w->key_ok.ensure(64));  // [0] key status, [32..63] RLC seed
+  HIP_TRY(w->key_tab.ensure(worker::KEY_SLOTS * 96 * 4));  // fixed size keeps the slots valid
+  const int kg = g2 ? 0 : 1;
+  int slot = -1, victim = 0;
+  for (int i = 0; i < worker::KEY_SLOTS; i++) {
+    const worker::key_slot& k = w->keys[i];
+    if (k.len == pk_len && k.g2 == kg && !memcmp(k.bytes, pk, pk_len)) slot = i;
+    if (k.used < w->keys[victim].used) victim = i;
+  }
+  if (slot < 0) {
+    slot = victim;
+    worker::key_slot& k = w->keys[slot];
+    k.len = 0;
     uint8_t ok = 0;
+    uint32_t* dst = w->key_tab.as<uint32_t>() + (size_t)slot * 96;
     HIP_TRY(hipMemcpyAsync(w->key_raw.p, pk, pk_len, hipMemcpyHostToDevice, st));
-    HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), w->key_aff.as<uint32_t>(), w->key_ok.as<uint8_t>(), st));
+    HIP_TRY(dh::launch_decode_key(g2 ? 0 : 1, w->key_raw.as<uint8_t>(), dst, w->key_ok.as<uint8_t>(), st));
     HIP_TRY(hipMemcpyAsync(&ok, w->key_ok.p, 1, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    memcpy(w->cached_key, pk, pk_len);
-    w->cached_key_len = pk_len;
-    w->cached_key_g2 = g2 ? 0 : 1;
-    w->cached_key_ok = ok;
+    memcpy(k.bytes, pk, pk_len);
+    k.len = pk_len;
+    k.g2 = kg;
+    k.ok = ok;
   }
-  if (w->cached_key_ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
+  w->keys[slot].used = ++w->key_clock;
+  w->key_cur = w->key_tab.as<uint32_t>() + (size_t)slot * 96;
+  if (w->keys[slot].ok != 1) return fail(DH_EKEY, "group public key is not a valid compressed subgroup point");
   return DH_OK;
 }
 
@@ -931,8 +953,8 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
       HIP_TRY(hipMemsetAsync(w->pass.p, 1, 1, st));
     } else {
       HIP_TRY(T.run(chk_names[std::min(level, 7)], [&] {
-        return group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups, w->key_aff.as<uint32_t>(),
-                           w->pass.as<uint8_t>(), st, w->key_aff.as<uint32_t>() + 48);
+        return group_check(w, g2, w->outA.as<uint32_t>(), w->outB.as<uint32_t>(), ngroups, w->key_cur, w->pass.as<uint8_t>(),
+                           st, w->key_cur + 48);
       }));
     }
     HIP_TRY(dh::launch_mark_groups(w->entries.as<uint32_t>(), m, gsize, w->pass.as<uint8_t>(), w->status.as<uint8_t>(),
@@ -972,7 +994,7 @@ int verify_core(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const u
   if (m > 0) {
     HIP_TRY(T.run("k_leaf_check", [&] {
       return leaf_check(w, g2, w->entries.as<uint32_t>(), m, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
-                        w->key_aff.as<uint32_t>(), w->status.as<uint8_t>(), d_verdict, st, w->key_aff.as<uint32_t>() + 48);
+                        w->key_cur, w->status.as<uint8_t>(), d_verdict, st, w->key_cur + 48);
     }));
     if (stats) stats[2] = m;
   }
@@ -1054,7 +1076,7 @@ int verify_small(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const 
   HIP_TRY(dh::launch_iota(w->entries.as<uint32_t>(), n, hs));
   HIP_TRY(TH.run("k_leaf_check", [&] {
     return leaf_check(w, g2, w->entries.as<uint32_t>(), n, w->sig_aff.as<uint32_t>(), w->q_pts.as<uint32_t>(),
-                      w->key_aff.as<uint32_t>(), w->status.as<uint8_t>(), d_verdict, hs, w->key_aff.as<uint32_t>() + 48);
+                      w->key_cur, w->status.as<uint8_t>(), d_verdict, hs, w->key_cur + 48);
   }));
   if (fork) HIP_TRY(hipStreamWaitEvent(hs, w->ev_sub, 0));
   HIP_TRY(dh::launch_and_subgroup(n, w->sub_bad.as<uint8_t>(), d_verdict, hs));
@@ -1402,7 +1424,6 @@ int recover_core(worker* w, int scheme, const uint8_t* commits, int t, int n_nod
     // group key = commit 0 (affine, key group) — staged where the group check expects it
     HIP_TRY(w->key_aff.ensure(96 * 4));
     HIP_TRY(hipMemcpyAsync(w->key_aff.p, w->r_caff.p, kaw * 4, hipMemcpyDeviceToDevice, st));
-    w->cached_key_len = 0;  // key_aff now holds this call's key
     dh::msm_geom g = geom_for(n_rounds, parts);
     g.half_stride = (uint32_t)n_rounds;
     dh::msm_ws ws{};
@@ -1823,7 +1844,7 @@ static int queue_node_check(worker* w, bool g2, const uint8_t* pk, size_t pk_len
   uint32_t* sA = w->node_sum.as<uint32_t>();
   uint8_t* res = w->node_res.as<uint8_t>();
   HIP_TRY(dh::launch_sum_partials(g2, (const uint32_t*)d_partials, k, partial_words(g2), sA, sA + jw, res, ts));
-  HIP_TRY(group_check(w, g2, sA, sA + jw, 1, w->key_aff.as<uint32_t>(), res + 1, ts, w->key_aff.as<uint32_t>() + 48));
+  HIP_TRY(group_check(w, g2, sA, sA + jw, 1, w->key_cur, res + 1, ts, w->key_cur + 48));
   return DH_OK;
 }
 
@@ -2123,7 +2144,6 @@ int dh_hash_to_curve(int group, const uint8_t* msgs, const uint32_t* msg_off, si
   if (total) HIP_TRY(hipMemcpyAsync(w->in_sigs.p, msgs + msg_off[0], total, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(w->in_prev_lens.p, off.data(), (n + 1) * 4, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(w->key_raw.p, dst, dst_len, hipMemcpyHostToDevice, st));
-  w->cached_key_len = 0;  // key_raw reused as the DST buffer
   HIP_TRY(dh::launch_h2c_generic(group == 2, w->in_sigs.as<uint8_t>(), w->in_prev_lens.as<uint32_t>(), n,
                                  w->key_raw.as<uint8_t>(), (uint32_t)dst_len, w->h2c_tmp.as<uint8_t>(), stride,
                                  w->out_rand.as<uint8_t>(), st));

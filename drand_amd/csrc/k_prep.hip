@@ -244,26 +244,53 @@ __global__ __launch_bounds__(256) void k_scalars(const uint32_t* __restrict__ se
   scal[i] = r;
 }
 
-// ---------------------------------------------------------------- key decode (one thread)
+// ---------------------------------------------------------------- key decode
+// Thread 0 decodes the point (square root, no subgroup test), then two waves run side by side: wave 0's first lane the
+// subgroup test, wave 1's first lane (G2 keys: the G1-signature schemes) [h_eff] pk, so the batch check can read
+// e([h_eff] B, pk) as e(B, [h_eff] pk) and skip the per-check cofactor clearing (k_vm_prep_groups). One lane did all
+// three in a row: 6.8 ms for a G2 key (k_decode_key<fp2>, profiles/r06/rocprof_single_beacon_r06d.csv), the cost
+// of a key-cache miss.
 template <class K>
-__global__ void k_decode_key(const uint8_t* __restrict__ pk, uint32_t* __restrict__ key_aff, uint8_t* __restrict__ ok) {
-  if (gtid() != 0) return;
-  aff<K> a;
-  uint8_t st;
-  if constexpr (sizeof(K) == sizeof(fp)) st = g1_decompress(a, pk, true);
-  else st = g2_decompress(a, pk, true);
-  *ok = st;
-  if (st != DEC_OK) {
-    a.x = K{};
-    a.y = K{};
+__global__ __launch_bounds__(128) void k_decode_key(const uint8_t* __restrict__ pk, uint32_t* __restrict__ key_aff,
+                                                    uint8_t* __restrict__ ok) {
+  __shared__ int st_sh, sub_sh;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    aff<K> a;
+    uint8_t st;
+    if constexpr (sizeof(K) == sizeof(fp)) st = g1_decompress(a, pk, false);
+    else st = g2_decompress(a, pk, false);
+    if (st != DEC_OK) {
+      a.x = K{};
+      a.y = K{};
+    }
+    st_aff_aos<K>(key_aff, 0, a);
+    st_sh = st;
+    sub_sh = 1;
   }
-  st_aff_aos<K>(key_aff, 0, a);
+  __syncthreads();
+  const bool dec_ok = st_sh == DEC_OK;
+  if (t == 0 && dec_ok) {
+    bool in;
+    if constexpr (sizeof(K) == sizeof(fp)) in = g1_in_subgroup28([&] { return ld_aff_aos<fp>(key_aff, 0); });
+    else in = g2_in_subgroup28([&] { return ld_aff_aos<fp2>(key_aff, 0); });
+    sub_sh = in ? 1 : 0;
+  }
   if constexpr (sizeof(K) == sizeof(fp2)) {
-    // G1-signature schemes: also [h_eff] pk (h_eff = 1 - z = |z| + 1), so the batch check can read
-    // e([h_eff] B, pk) as e(B, [h_eff] pk) and skip the per-check cofactor clearing (k_vm_prep_groups)
-    aff<fp2> h = a;
-    if (st == DEC_OK) h = jac_to_aff(jac_add(jac_mul_uabs(a), jac_from_aff(a)));
-    st_aff_aos<fp2>(key_aff, 1, h);
+    if (t == 64) {
+      aff<fp2> h{fp2{}, fp2{}};
+      if (dec_ok) {
+        const aff<fp2> a = ld_aff_aos<fp2>(key_aff, 0);
+        h = jac_to_aff(jac_add(jac_mul_uabs(a), jac_from_aff(a)));  // G1's h_eff = 1 - z = |z| + 1, applied to pk
+      }
+      st_aff_aos<fp2>(key_aff, 1, h);
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    const uint8_t st = (uint8_t)st_sh == DEC_OK && !sub_sh ? (uint8_t)DEC_BAD : (uint8_t)st_sh;
+    *ok = st;
+    if (st != DEC_OK) st_aff_aos<K>(key_aff, 0, aff<K>{K{}, K{}});
   }
 }
 
@@ -287,8 +314,8 @@ hipError_t launch_scalars(const uint32_t* seed_words, size_t n, const uint8_t* s
 }
 
 hipError_t launch_decode_key(int key_g2, const uint8_t* pk, uint32_t* key_aff, uint8_t* ok, hipStream_t st) {
-  if (key_g2) hipLaunchKernelGGL(k_decode_key<fp2>, dim3(1), dim3(64), 0, st, pk, key_aff, ok);
-  else hipLaunchKernelGGL(k_decode_key<fp>, dim3(1), dim3(64), 0, st, pk, key_aff, ok);
+  if (key_g2) hipLaunchKernelGGL(k_decode_key<fp2>, dim3(1), dim3(128), 0, st, pk, key_aff, ok);
+  else hipLaunchKernelGGL(k_decode_key<fp>, dim3(1), dim3(128), 0, st, pk, key_aff, ok);
   return hipGetLastError();
 }
 

@@ -8,8 +8,10 @@
     subsets (with invalid partials and rounds short of t valid ones), pinned by [f(0)] H(m).
 The rejected set must be exactly the corrupted one; the CPU oracle (oracle/, test infrastructure) re-verifies every
 rejected round and a sample of accepted ones (crypto/schemes.go:70-72 restated), and Recover on a sample of rounds
-(chain/beacon/chainstore.go:202-207 restated). configs[4] (4M chained replay) keeps its 16k-round real-chain test
-(test_gpu_paths.py::test_chained_replay_real_chain): signing a sequential 4M chain takes minutes.
+(chain/beacon/chainstore.go:202-207 restated). configs[4] (4M chained replay at 0.1%) runs here at 262,144 rounds,
+twice, so the second call takes the dense-fault shape (level 0 skipped, the 256 -> 32 -> 4 ladder); the 16k-round
+1% real-chain test (test_gpu_paths.py::test_chained_replay_real_chain) stays beside it; signing a sequential 4M chain
+takes minutes, so the full size is the bench's (bench/bench_configs.py chained).
 """
 import ctypes
 import hashlib
@@ -229,3 +231,60 @@ def test_config4_tbls_recover_100k(dh, oracle, subsets):
         assert (w is not None) == bool(ok[j]), j
         if w is not None:
             assert w == sigs[j].tobytes(), j
+
+
+def test_config5_chained_replay_262k_dense(dh, oracle):
+    """BASELINE configs[4]'s shape at 262,144 rounds (a quarter of one 1M window; the 4M chain's signing takes ~3.5
+    minutes and stays in the bench, profiles/r06/config_chained_*.json): a sequential pedersen-bls-chained chain, 0.1%
+    of its rounds corrupted in the three Cfg5 classes, replayed twice through dh_verify_batch_device as
+    CheckPastBeacons does, one call per window. The first call fails level 0 and bisects 1024 -> ...; its first level's
+    failure rate (~1 fault per 1000 rounds) marks the worker dense, so the second call skips level 0 and runs the
+    dense ladder 256 -> 32 -> 4 -> leaves (drandhip.cpp skip0, next_group_size) — the shape the 16k-round 1% test
+    never reaches. Both calls must reject exactly U{k, k+1} (/root/reference/chain/beacon/sync_manager.go:191-225;
+    core/drand_test.go:1105-1111's faulty-round contract), which the oracle confirms on every rejected round and 2,000
+    accepted ones."""
+    import torch
+    import chainsynth
+    from drand_amd import _lib
+    lib = _lib.load()
+    name = "pedersen-bls-chained"
+    s = dh.scheme_from_name(name)
+    sk = _secret(name)
+    pk = s.public_key(sk)
+    n = 1 << 18
+    genesis = hashlib.sha256(b"drandhip-genesis").digest()
+    bad = chainsynth.corrupted_rounds(n, n // 1000)
+    sigs = chainsynth.sign_chain(s, sk, 1, n, genesis, bad, np.random.default_rng(0xC5))
+    chainsynth.corrupt(sigs, bad, random.Random(31))
+    prev, plen = chainsynth.stored_prevs(sigs, genesis)
+    rounds = np.arange(1, n + 1, dtype=np.uint64)
+    expected = chainsynth.expected_faulty(bad, n)
+    dev = torch.device("cuda")
+    d_r = torch.from_numpy(rounds.view(np.int64)).to(dev)
+    d_s = torch.from_numpy(sigs).to(dev)
+    d_p = torch.from_numpy(np.concatenate([prev.reshape(-1), np.zeros(4, np.uint8)])).to(dev)
+    d_l = torch.from_numpy(plen.astype(np.uint32).view(np.int32)).to(dev)
+    d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    levels = []
+    for seed in (91, 92):
+        st = (ctypes.c_uint64 * 4)()
+        rc = lib.dh_verify_batch_device(s.id, pk, len(pk), ctypes.c_void_p(d_r.data_ptr()), ctypes.c_void_p(d_s.data_ptr()),
+                                        96, ctypes.c_void_p(d_p.data_ptr()), prev.shape[1], ctypes.c_void_p(d_l.data_ptr()),
+                                        n, ctypes.c_void_p(d_v.data_ptr()), None, seed, None, st)
+        assert rc == 0, _lib.last_error()
+        v = d_v.cpu().numpy().astype(bool)
+        assert np.flatnonzero(~v).tolist() == expected.tolist()
+        assert st[3] == len(expected)
+        levels.append(list(st))
+    # call 1: level 0 + at least the 1024-group level; call 2: no level 0 (the dense worker's hint), >= 3 levels
+    assert levels[0][0] >= 3 and levels[0][1] >= 1 and levels[1][0] >= 3 and levels[1][2] > 0, levels
+    ov = np.zeros(0)
+    samp = np.unique(np.concatenate([expected, np.random.default_rng(5).choice(np.flatnonzero(v), 2000, replace=False)]))
+    ov = np.zeros(len(samp), np.uint8)
+    rs, ss = np.ascontiguousarray(rounds[samp]), np.ascontiguousarray(sigs[samp])
+    ps, ls = np.ascontiguousarray(prev[samp]), np.ascontiguousarray(plen[samp].astype(np.uint32))
+    oracle.lib().or_verify_batch(oracle.sid(name), pk, len(pk), rs.ctypes.data, ss.ctypes.data, 96, ps.ctypes.data,
+                                 prev.shape[1], ls.ctypes.data, len(samp), 16, ov.ctypes.data, None)
+    assert ov.astype(bool).tolist() == v[samp].tolist()
+    print("bisection stats per call:", levels)
