@@ -631,9 +631,20 @@ static size_t np2c_max_leaves() {
   return v;
 }
 
+// G1-signature checks with [h_eff] pk at hand take their G1 sides in Jacobian form (NP2J: no prep kernel, no
+// inversion before the program); DRANDHIP_G1_JAC=0 keeps the affine prep (k_vm_prep_groups / _leaves) for A/B runs
+static bool g1_jac() {
+  static const bool v = [] {
+    const char* e = getenv("DRANDHIP_G1_JAC");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 static hipError_t group_check(worker* w, bool g2, const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key,
                               uint8_t* pass, hipStream_t st, const uint32_t* key_h = nullptr) {
   if (lane_pairing()) return dh::launch_group_check(g2, A, B, ngroups, key, pass, st);
+  if (!g2 && key_h && g1_jac()) return dh::launch_group_check_g1j(A, B, ngroups, key_h, pass, st);
   hipError_t e;
   if (g2 && ngroups <= np2c_max_groups()) {
     if ((e = w->vm_pairs.ensure(ngroups * dh::group_check_c_pair_words() * 4)) != hipSuccess) return e;
@@ -653,6 +664,7 @@ static hipError_t leaf_check(worker* w, bool g2, const uint32_t* entries, size_t
                              const uint32_t* q_pts, const uint32_t* key, const uint8_t* status, uint8_t* verdict,
                              hipStream_t st, const uint32_t* key_h = nullptr) {
   if (lane_pairing()) return dh::launch_leaf_check(g2, entries, m, sig_aff, q_pts, key, status, verdict, st);
+  if (!g2 && key_h && g1_jac()) return dh::launch_leaf_check_g1j(entries, m, sig_aff, q_pts, key_h, status, verdict, st);
   hipError_t e;
   if (g2 && m <= np2c_max_leaves()) {
     if ((e = w->vm_pairs.ensure(m * dh::group_check_c_pair_words() * 4)) != hipSuccess) return e;
@@ -1045,7 +1057,7 @@ int verify_small(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const 
   HIP_TRY(w->sig_aff.ensure(n * aw * 4));
   HIP_TRY(w->q_pts.ensure(n * jw * 4));
   HIP_TRY(w->entries.ensure(n * 4));
-  HIP_TRY(w->h2c_tmp.ensure(dh::hash_tmp_bytes(g2, n)));
+  HIP_TRY(w->h2c_tmp.ensure(dh::hash_small_tmp_bytes(g2, n)));
   const bool chained = scheme == DH_SCHEME_CHAINED && d_prevs && !d_msgs32;
   const bool fork = w->tail && !(chained && d_prev_lens && !lens_checked);
   HIP_TRY(w->sub_bad.ensure(n));
@@ -1063,8 +1075,8 @@ int verify_small(worker* w, int scheme, const uint8_t* pk, size_t pk_len, const 
   }));
   if (fork) HIP_TRY(hipEventRecord(w->ev_dec, st));
   HIP_TRY(TH.run(d_msgs32 ? (g2 ? "k_prep_msg32<fp2>" : "k_prep_msg32<fp>") : (g2 ? "k_prep_msg<fp2>" : "k_prep_msg<fp>"), [&] {
-    return dh::launch_hash(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, d_msgs32, n, chained ? 1 : 0, dst_id(scheme),
-                           fork ? nullptr : w->status.as<uint8_t>(), w->q_pts.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), hs);
+    return dh::launch_hash_small(g2, d_rounds, d_prevs, prev_stride, d_prev_lens, d_msgs32, n, chained ? 1 : 0, dst_id(scheme),
+                                 fork ? nullptr : w->status.as<uint8_t>(), w->q_pts.as<uint32_t>(), w->h2c_tmp.as<uint32_t>(), hs);
   }));
   HIP_TRY(T.run(g2 ? "k_sub_sig_small<fp2>" : "k_sub_sig_small<fp>", [&] {
     return dh::launch_sub_flag(g2, n, w->status.as<uint8_t>(), w->sig_aff.as<uint32_t>(), w->sub_bad.as<uint8_t>(), st);

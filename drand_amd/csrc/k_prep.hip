@@ -124,6 +124,60 @@ __global__ __launch_bounds__(64) void k_and_subgroup(size_t n, const uint8_t* __
   if (sub_bad[i]) verdict[i] = 0;
 }
 
+// small-batch path, G1 hash in three launches, as the G2 hash runs (k_h2f_g2 -> k_sswu_g2 -> k_add_iso_g2): the
+// round's two SSWU maps (each a square-root exponentiation, the bulk of the hash) run in two workgroups of their own,
+// so on two SIMDs side by side, instead of one after the other on one lane (k_prep_msg_g1). Two waves of ONE
+// workgroup measured no faster (1.24 ms against 1.1: they shared a SIMD, and a dependent MAD chain needs one SIMD's
+// issue slots to itself). The hash is the small path's critical step for G1 signatures (decode 0.44-0.57 ms beside it).
+// tmp: per round u0, u1 (2 x 12 words), then the two SSWU points (2 x 36 words) — hash_small_tmp_bytes.
+__global__ __launch_bounds__(64) void k_h2f_g1_small(const uint64_t* __restrict__ rounds, const uint8_t* __restrict__ prevs,
+                                                     size_t prev_stride, const uint32_t* __restrict__ prev_lens,
+                                                     const uint8_t* __restrict__ msgs32, size_t n, int chained, int dst_id,
+                                                     uint8_t* __restrict__ status, uint32_t* __restrict__ u_out) {
+  const size_t i = gtid();
+  if (i >= n) return;
+  const sha_h d = message_of(rounds, prevs, prev_stride, prev_lens, msgs32, chained, i, status);
+  uint32_t b[4][8];
+  xmd32<4>(b, d, dst_id);
+  st_f<fp>(u_out + 24 * i, fp_from_be512(b[0], b[1]));
+  st_f<fp>(u_out + 24 * i + 12, fp_from_be512(b[2], b[3]));
+}
+
+// one SSWU map per workgroup (lane 0): map j of round j / 2
+__global__ __launch_bounds__(64) void k_sswu_g1_small(const uint32_t* __restrict__ u, size_t m, uint32_t* __restrict__ pts) {
+  const size_t j = blockIdx.x;
+  if (j >= m || threadIdx.x) return;
+  fp x;
+  ld_f<fp>(x, u + 12 * j);
+  st_jac_aos<fp>(pts, j, swu_jac(sswu_g1(x)));
+}
+
+__global__ __launch_bounds__(64) void k_add_iso_g1_small(const uint32_t* __restrict__ pts, size_t n, uint32_t* __restrict__ q_out) {
+  const size_t i = gtid();
+  if (i >= n) return;
+  const jac<fp> p0 = ld_jac_aos<fp>(pts, 2 * i), p1 = ld_jac_aos<fp>(pts, 2 * i + 1);
+  jac<fp> s;
+  const jac<fp> q = jac_add_distinct(s, p0, p1) ? iso11_jac(s) : jac_add(iso11_jac(p0), iso11_jac(p1));
+  st_jac_aos<fp>(q_out, i, q);
+}
+
+size_t hash_small_tmp_bytes(int sig_g2, size_t n) {
+  return sig_g2 ? hash_tmp_bytes(1, n) : n * (24 + 72) * 4;
+}
+
+hipError_t launch_hash_small(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
+                             const uint8_t* msgs32, size_t n, int chained, int dst_id, uint8_t* status, uint32_t* q_out,
+                             uint32_t* tmp, hipStream_t st) {
+  if (!n) return hipSuccess;
+  if (sig_g2) return launch_hash(1, rounds, prevs, prev_stride, prev_lens, msgs32, n, chained, dst_id, status, q_out, tmp, st);
+  uint32_t* pts = tmp + 24 * n;
+  hipLaunchKernelGGL(k_h2f_g1_small, dim3(nblk(n, 64)), dim3(64), 0, st, rounds, prevs, prev_stride, prev_lens, msgs32, n,
+                     chained, dst_id, status, tmp);
+  hipLaunchKernelGGL(k_sswu_g1_small, dim3((unsigned)(2 * n)), dim3(64), 0, st, (const uint32_t*)tmp, 2 * n, pts);
+  hipLaunchKernelGGL(k_add_iso_g1_small, dim3(nblk(n, 64)), dim3(64), 0, st, (const uint32_t*)pts, n, q_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_dec_sig(int sig_g2, const uint8_t* sigs, size_t stride, size_t n, uint8_t* status, uint32_t* sig_aff,
                           uint8_t* rand_out, hipStream_t st) {
   if (!n) return hipSuccess;

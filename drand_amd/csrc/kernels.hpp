@@ -70,6 +70,12 @@ hipError_t launch_dec_sig(int sig_g2, const uint8_t* sigs, size_t stride, size_t
                           uint8_t* rand_out, hipStream_t st);
 hipError_t launch_sub_flag(int sig_g2, size_t n, const uint8_t* status, const uint32_t* sig_aff, uint8_t* sub_bad, hipStream_t st);
 hipError_t launch_and_subgroup(size_t n, const uint8_t* sub_bad, uint8_t* verdict, hipStream_t st);
+// small-batch path: launch_hash with the G1 hash's two SSWU maps in workgroups of their own (G2: launch_hash);
+// tmp: hash_small_tmp_bytes
+size_t hash_small_tmp_bytes(int sig_g2, size_t n);
+hipError_t launch_hash_small(int sig_g2, const uint64_t* rounds, const uint8_t* prevs, size_t prev_stride, const uint32_t* prev_lens,
+                             const uint8_t* msgs32, size_t n, int chained, int dst_id, uint8_t* status, uint32_t* q_out,
+                             uint32_t* tmp, hipStream_t st);
 // hash points Q_i (before cofactor clearing) of the beacon digests of (rounds, prevs) or of the given 32-byte
 // msgs32; a chained record longer than its slot marks status[i] = DEC_BAD. tmp: hash_tmp_bytes(sig_g2, n).
 size_t hash_tmp_bytes(int sig_g2, size_t n);
@@ -133,6 +139,13 @@ hipError_t launch_leaf_check_vm(int sig_g2, const uint32_t* entries, size_t m, c
 hipError_t launch_leaf_check_vm_c(const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
                                   const uint32_t* key_aff, const uint8_t* status, uint32_t* pairs, uint8_t* live, uint8_t* done,
                                   uint8_t* verdict, hipStream_t st);
+
+// G1-signature checks on Jacobian G1 sides (NP2J, no prep kernel): groups (A, B Jacobian AoS) and leaves;
+// key_h = [h_eff] pk (affine)
+hipError_t launch_group_check_g1j(const uint32_t* A, const uint32_t* B, size_t ngroups, const uint32_t* key_h, uint8_t* pass,
+                                  hipStream_t st);
+hipError_t launch_leaf_check_g1j(const uint32_t* entries, size_t m, const uint32_t* sig_aff, const uint32_t* q_pts,
+                                 const uint32_t* key_h, const uint8_t* status, uint8_t* verdict, hipStream_t st);
 
 hipError_t launch_multi_pairing_vm(const uint32_t* P, const uint32_t* Q, size_t n, uint32_t* pairs, uint8_t* live,
                                    uint32_t* f_tmp, uint8_t* pass, hipStream_t st);

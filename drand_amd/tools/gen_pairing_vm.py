@@ -390,6 +390,20 @@ def ml_add(T, Q):
 
 
 def miller_loop(Ps, Qs):
+    """Ps: affine (x, y), or Jacobian (X, Y, Z): then every line is scaled by Z^3, an Fp factor the final
+    exponentiation removes (c2 Z^3, c1 X Z, c0 Y for c2, c1 x, c0 y), so a check needs no inversion for its G1 side."""
+    ev = []
+    for P in Ps:
+        if len(P) == 3:
+            X, Y, Z = P
+            ev.append((X * Z, Y, (Z * Z) * Z))
+        else:
+            ev.append((P[0], P[1], None))
+
+    def line(f, k, c0, c1, c2):
+        px, py, z3 = ev[k]
+        return f.mul_line(c2 if z3 is None else c2.mul_fp(z3), c1.mul_fp(px), c0.mul_fp(py))
+
     f = F12.one()
     T = [(Q[0], Q[1], F2(L.const(1), L())) for Q in Qs]
     started = False
@@ -399,11 +413,11 @@ def miller_loop(Ps, Qs):
         started = True
         for k in range(len(Ps)):
             T[k], (c0, c1, c2) = ml_dbl(T[k])
-            f = f.mul_line(c2, c1.mul_fp(Ps[k][0]), c0.mul_fp(Ps[k][1]))
+            f = line(f, k, c0, c1, c2)
         if (U_ABS >> b) & 1:
             for k in range(len(Ps)):
                 T[k], (c0, c1, c2) = ml_add(T[k], Qs[k])
-                f = f.mul_line(c2, c1.mul_fp(Ps[k][0]), c0.mul_fp(Ps[k][1]))
+                f = line(f, k, c0, c1, c2)
         f = f.mat()
     return f.conj()
 
@@ -533,6 +547,8 @@ def build_tag(tag):
     global PROG
     if tag == "NP2C":
         return build_np2c()
+    if tag.startswith("NP") and tag.endswith("J"):
+        return build(int(tag[2:-1]), jac=True)
     if tag.startswith("NP"):
         return build(int(tag[2:]))
     PROG = Prog()
@@ -558,15 +574,17 @@ def build_tag(tag):
     return prog, outs
 
 
-def build(np_):
+def build(np_, jac=False):
+    """NP1 / NP2: np_ pairs with affine P; NP1J / NP2J (jac): P Jacobian (P%d.x, .y, .z), for the G1-signature checks,
+    whose G1 sides are RLC sums and hash points in Jacobian form (no inversion before the program)."""
     global PROG
     PROG = Prog()
     Ps, Qs = [], []
     for k in range(np_):
-        px, py = L.node(PROG.inp("P%d.x" % k)), L.node(PROG.inp("P%d.y" % k))
+        P = tuple(L.node(PROG.inp("P%d.%s" % (k, c))) for c in ("xyz" if jac else "xy"))
         qx = F2(L.node(PROG.inp("Q%d.x0" % k)), L.node(PROG.inp("Q%d.x1" % k)))
         qy = F2(L.node(PROG.inp("Q%d.y0" % k)), L.node(PROG.inp("Q%d.y1" % k)))
-        Ps.append((px, py))
+        Ps.append(P)
         Qs.append((qx, qy))
     r = final_exp(miller_loop(Ps, Qs))
     outs = []
@@ -811,10 +829,12 @@ def validate_np2c(prog, outs, phases, slot, nslots):
 def validate(np_, prog, outs, phases, slot, nslots):
     if np_ == "NP2C":
         return validate_np2c(prog, outs, phases, slot, nslots)
+    jac = False
     if isinstance(np_, str):
         if not np_.startswith("NP"):
             return  # checked in validate_split
-        np_ = int(np_[2:])
+        jac = np_.endswith("J")
+        np_ = int(np_[2:].rstrip("J"))
     B = _bls_points()
     rng = random.Random(1)
     one = [1] + [0] * 11
@@ -822,6 +842,12 @@ def validate(np_, prog, outs, phases, slot, nslots):
     def run(pairs):
         inp = {}
         for k, (Pt, Qt) in enumerate(pairs):
+            if jac:  # the same point with a random Z: X = x Z^2, Y = y Z^3
+                z = rng.randrange(1, P)
+                inp["P%d.x" % k], inp["P%d.y" % k], inp["P%d.z" % k] = Pt[0] * z * z % P, Pt[1] * z * z * z % P, z
+                inp["Q%d.x0" % k], inp["Q%d.x1" % k] = Qt[0]
+                inp["Q%d.y0" % k], inp["Q%d.y1" % k] = Qt[1]
+                continue
             inp["P%d.x" % k], inp["P%d.y" % k] = Pt[0], Pt[1]
             inp["Q%d.x0" % k], inp["Q%d.x1" % k] = Qt[0]
             inp["Q%d.y0" % k], inp["Q%d.y1" % k] = Qt[1]
@@ -914,7 +940,7 @@ def emit(progs):
     return "\n".join(lines)
 
 
-TAGS = ("NP1", "NP2", "ML1", "MUL12", "FE", "NP2C")
+TAGS = ("NP1", "NP2", "ML1", "MUL12", "FE", "NP2C", "NP1J", "NP2J")
 
 
 def build_all():
