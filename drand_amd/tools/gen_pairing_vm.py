@@ -34,7 +34,7 @@ import gen_consts as gc  # noqa: E402
 P = gc.P
 U_ABS = -gc.U
 MAXT = 15        # terms per product operand (two operands share one op record)
-MAXT_LIN = 31    # terms per LIN op (the record's words 1..31)
+MAXT_LIN = 30    # terms per LIN op (the record's words 1..15 and 17..31: two halves, one per lane of a lane pair)
 MAXC = 32767     # |coefficient| per term (16-bit signed field of a term word)
 LANES = 64
 RP = 1 << 392    # the VM's Montgomery radix (k_vm.hip: 14 x 28-bit limbs)
@@ -871,7 +871,7 @@ def validate(np_, prog, outs, phases, slot, nslots):
 
 
 # ----------------------------------------------------------------------------------------- emission
-REC = 32  # words per op record: header, MAXT A terms, MAXT B terms (fixed positions), padding; LIN: MAXT_LIN A terms
+REC = 32  # words per op record: header, MAXT A terms, half header, MAXT B terms (LIN: its terms in the two halves)
 
 
 def c_fp28(v):
@@ -884,10 +884,13 @@ def emit(progs):
     """progs: list of (np, prog, outs, phases, slot, nslots).
 
     Layout read by k_vm.hip: PHASES[2 * ph] = kind | cnt << 8, PHASES[2 * ph + 1] = index of the phase's first op;
-    op k of phase ph is the REC-word record OPS[REC * (first + k) ...]: word 0 = dst slot | na << 16 | nb << 24,
-    words 1..MAXT = A terms, words 1+MAXT..2*MAXT = B terms (a LIN op: words 1..MAXT_LIN = A terms), a term =
-    slot | (coeff & 0xffff) << 16. Constants are emitted in the VM's representation (c_fp28)."""
-    assert 1 + 2 * MAXT <= REC and 1 + MAXT_LIN <= REC
+    op k of phase ph is the REC-word record OPS[REC * (first + k) ...] in two 16-word halves: word 0 = dst slot |
+    na << 16 | nb << 24, words 1..na = the first half's terms; word 16 = nb << 16, words 17..16+nb = the second half's
+    terms. A product's halves are its operands A and B, a LIN op's the first MAXT of its terms and the rest; a term =
+    slot | (coeff & 0xffff) << 16. k_vm.hip runs a phase of at most 32 ops on lane pairs, each lane reading one half
+    (its count at bits 16..23 of the half's first word), and a wider phase one op per lane over both halves.
+    Constants are emitted in the VM's representation (c_fp28)."""
+    assert 2 * (1 + MAXT) == REC and MAXT_LIN == 2 * MAXT
     lines = ["// generated by drand_amd/tools/gen_pairing_vm.py — do not edit",
              "// Lane-parallel multi-pairing check programs (see the generator's docstring).",
              "#pragma once", "#include <stdint.h>", "", "namespace dh {", "namespace vm {", ""]
@@ -909,14 +912,18 @@ def emit(progs):
                 a = n["a"]
                 b = n.get("b", [])
                 assert len(a) <= (MAXT_LIN if kind == "lin" else MAXT) and len(b) <= MAXT
+                if kind == "lin":
+                    a, b = a[:MAXT], a[MAXT:]
                 rec = [0] * REC
                 rec[0] = slot[i] | (len(a) << 16) | (len(b) << 24)
+                rec[1 + MAXT] = len(b) << 16
                 for k, (s_, c) in enumerate(a):
                     rec[1 + k] = slot[s_] | ((c & 0xffff) << 16)
                 for k, (s_, c) in enumerate(b):
-                    rec[1 + MAXT + k] = slot[s_] | ((c & 0xffff) << 16)
+                    rec[2 + MAXT + k] = slot[s_] | ((c & 0xffff) << 16)
                 op_words += rec
                 nops += 1
+        op_words += [0] * (REC // 2)  # pad: k_vm.hip's record loads read a full record from a pair lane's half
         ins = [slot[i] for i in prog.inputs]
         consts = [(slot[n], v) for v, n in prog.consts.items() if n in slot]
         tag = np_ if isinstance(np_, str) else "NP%d" % np_
