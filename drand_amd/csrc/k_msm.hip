@@ -807,6 +807,32 @@ DH_DEV typename C::P add_lds(const typename C::P& a, const uint32_t* buf, int nt
     return C::template addx<EXACT>(a, lds_get_pt<C>(buf, nthr, i));
   }
 }
+// The sum of cnt stored points p[0 .. cnt) (rowtree: a lane's serial run of G segment values), or, with three
+// arguments, of the points first + k for k = lane, lane + 64, ... < parts (rowred: a row's wave partials). EXACT = false
+// takes the additions without their exceptional-case tests; a poisoned result (Z = 0 without the infinity flag, which
+// every later fast addition keeps) is recomputed with the exact formulas by the caller, so the loop body holds one
+// formula (r05 checked and redid each addition in the loop: both formulas and the old sum live at once, the G2 row tree
+// ~2,500 scratch instructions per step)
+template <class C, bool EXACT>
+DH_DEV typename C::P run_mem(const uint32_t* __restrict__ p, uint32_t cnt) {
+  typename C::P acc = C::inf();
+#pragma unroll 1
+  for (uint32_t k = 0; k < cnt; k++) acc = C::template add_mem<EXACT>(acc, p + (size_t)3 * C::EW * k);
+  return acc;
+}
+template <class C, bool EXACT>
+DH_DEV typename C::P run_mem(const uint32_t* __restrict__ base, size_t first, uint32_t parts) {
+  typename C::P acc = C::inf();
+#pragma unroll 1
+  for (uint32_t k = threadIdx.x; k < parts; k += 64) acc = C::template add_mem<EXACT>(acc, base + (size_t)3 * C::EW * (first + k));
+  return acc;
+}
+// the exact sum of the two points parked in LDS slots i and j, out of line: the fast tree step that calls it on a
+// poisoned sum (never for honest inputs) keeps none of its registers
+template <class C>
+__attribute__((noinline)) DH_DEV typename C::P add_lds_exact(const uint32_t* buf, int nthr, int i, int j) {
+  return add_lds<C, true>(lds_get_pt<C>(buf, nthr, i), buf, nthr, j);
+}
 // the tree over aligned runs of `span` lanes (a power of two <= 64) of each wave: lane l, l % span == 0, ends with the
 // sum of lanes [l, l + span). Every thread of the workgroup calls it (barriers); buf: lds_words<C>() x blockDim words.
 // The inputs are exact (stored points), so a poisoned sum is recomputed with the exact formulas on the spot.
@@ -815,19 +841,25 @@ DH_DEV typename C::P wave_tree(typename C::P acc, uint32_t* buf, uint32_t span) 
   const int nthr = blockDim.x, i = threadIdx.x, lane = i & 63;
 #pragma unroll 1
   for (uint32_t step = 1; step < span; step <<= 1) {
-    if ((lane & (2 * step - 1)) == step) lds_put_pt<C>(buf, nthr, i, acc);  // only the lanes read at this step
+    // every lane still holding a partial sum parks it: its partner reads it, and a poisoned sum is redone from the
+    // two parked operands, so the lane's own sum is not live across the fast addition
+    if ((lane & (step - 1)) == 0) lds_put_pt<C>(buf, nthr, i, acc);
     __syncthreads();
     if ((lane & (2 * step - 1)) == 0) {
       typename C::P s = add_lds<C, false>(acc, buf, nthr, i + (int)step);
-      acc = C::poisoned(s) ? add_lds<C, true>(acc, buf, nthr, i + (int)step) : s;
+      if (C::poisoned(s)) {
+        if constexpr (C::PARTS == 4) s = add_lds_exact<C>(buf, nthr, i, i + (int)step);
+        else s = add_lds<C, true>(lds_get_pt<C>(buf, nthr, i), buf, nthr, i + (int)step);  // G1: a call would cost
+      }                                                                                        // the second wave/SIMD
+      acc = s;
     }
     __syncthreads();
   }
   return acc;
 }
 
-template <class C>
-__global__ __launch_bounds__(256, C::OCC) void k_msm_segsum28(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ off,
+template <class C, bool FEW = false>
+__global__ __launch_bounds__(FEW ? 64 : 256, FEW ? 1 : C::OCC) void k_msm_segsum28(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ off,
                                                               msm_geom g, size_t ngw, size_t rows_per_set, uint32_t* __restrict__ segs,
                                                               uint32_t* __restrict__ runs) {
   const size_t t = gtid();
@@ -844,25 +876,28 @@ __global__ __launch_bounds__(256, C::OCC) void k_msm_segsum28(const uint32_t* __
   stj28<C>(segs, t, tot);
   stj28<C>(runs, t, run);
 }
+// [k] run + tot, run and tot read from memory where the additions use them: the addend is not held in registers
+// across the doublings (G2: 84 fewer live registers; the addition's spills went from ~1,350 scratch instructions per
+// step to none)
 template <class C, bool EXACT>
-DH_DEV typename C::P seg_off(const typename C::P& run, uint32_t k, const uint32_t* __restrict__ tot) {
+DH_DEV typename C::P seg_off(const uint32_t* __restrict__ run, uint32_t k, const uint32_t* __restrict__ tot) {
   typename C::P acc = C::inf();
 #pragma unroll 1
   for (int bit = 31 - __builtin_clz(k); bit >= 0; bit--) {
     acc = C::dbl(acc);
-    if ((k >> bit) & 1) acc = C::template addx<EXACT>(acc, run);
+    if ((k >> bit) & 1) acc = C::template add_mem<EXACT>(acc, run);
   }
   return C::template add_mem<EXACT>(acc, tot);
 }
-template <class C>
-__global__ __launch_bounds__(256, C::OCC) void k_msm_segoff28(msm_geom g, size_t ngw, uint32_t* __restrict__ segs,
+template <class C, bool FEW = false>
+__global__ __launch_bounds__(FEW ? 64 : 256, FEW ? 1 : C::OCC) void k_msm_segoff28(msm_geom g, size_t ngw, uint32_t* __restrict__ segs,
                                                               const uint32_t* __restrict__ runs) {
   const size_t t = gtid();
   if (t >= ngw * g.nseg) return;
   const uint32_t k = (t % g.nseg) * g.seglen;  // a - 1
   if (!k) return;
-  const typename C::P run = ldj28<C>(runs, t);
-  if (run.inf) return;
+  const uint32_t* run = runs + (size_t)3 * C::EW * t;
+  if (ldj28<C>(runs, t).inf) return;  // run at infinity: the segment's value is tot as stored
   uint32_t* tot = segs + (size_t)3 * C::EW * t;
   typename C::P r = seg_off<C, false>(run, k, tot);
   if (C::poisoned(r)) r = seg_off<C, true>(run, k, tot);
@@ -878,8 +913,8 @@ __global__ __launch_bounds__(256, C::OCC) void k_msm_segoff28(msm_geom g, size_t
 // row sum in its first lane, or, for more than 64 lanes (a multiple of 64: fit_segments), one partial per wave that
 // k_msm_rowred28 (one wave per row) sums the same way. Measured against r04's launch tree on the tbls MSMs (64 groups of
 // 2 windows of 2,048 segments, gpurun_out r05w): the pure wave tree was 8.2 ms against 4.4.
-template <class C>
-__global__ __launch_bounds__(256, C::OCC) void k_msm_rowtree28(const uint32_t* __restrict__ segs, uint32_t nseg, uint32_t G,
+template <class C, bool FEW = false>
+__global__ __launch_bounds__(FEW ? 64 : 256, FEW ? 1 : C::OCC) void k_msm_rowtree28(const uint32_t* __restrict__ segs, uint32_t nseg, uint32_t G,
                                                                size_t ngw, uint32_t lpr, uint32_t span, uint32_t* __restrict__ out) {
   __shared__ uint32_t buf[lds_words<C>() * 256];
   const size_t t = gtid();
@@ -887,12 +922,10 @@ __global__ __launch_bounds__(256, C::OCC) void k_msm_rowtree28(const uint32_t* _
   if (t < ngw * lpr) {
     const size_t row = t / lpr;
     const uint32_t s0 = (uint32_t)(t % lpr) * G;
-#pragma unroll 1
-    for (uint32_t k = s0; k < s0 + G && k < nseg; k++) {
-      const uint32_t* p = segs + (size_t)3 * C::EW * (row * nseg + k);
-      const typename C::P sum = C::template add_mem<false>(acc, p);
-      acc = C::poisoned(sum) ? C::template add_mem<true>(acc, p) : sum;
-    }
+    const uint32_t* p = segs + (size_t)3 * C::EW * (row * nseg + s0);
+    const uint32_t cnt = s0 >= nseg ? 0 : min(G, nseg - s0);
+    acc = run_mem<C, false>(p, cnt);
+    if (C::poisoned(acc)) acc = run_mem<C, true>(p, cnt);
   }
   acc = wave_tree<C>(acc, buf, span);
   if (t < ngw * lpr && (t & (span - 1)) == 0) stj28<C>(out, t / span, acc);
@@ -902,12 +935,8 @@ __global__ __launch_bounds__(64) void k_msm_rowred28(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ rowsum) {
   __shared__ uint32_t buf[lds_words<C>() * 64];
   const size_t row = blockIdx.x;
-  typename C::P acc = C::inf();
-  for (uint32_t k = threadIdx.x; k < parts; k += 64) {
-    const uint32_t* p = parts_in + (size_t)3 * C::EW * (row * parts + k);
-    const typename C::P s = C::template add_mem<false>(acc, p);
-    acc = C::poisoned(s) ? C::template add_mem<true>(acc, p) : s;
-  }
+  typename C::P acc = run_mem<C, false>(parts_in, row * parts, parts);
+  if (C::poisoned(acc)) acc = run_mem<C, true>(parts_in, row * parts, parts);
   acc = wave_tree<C>(acc, buf, span);
   if (threadIdx.x == 0) stj28<C>(rowsum, row, acc);
 }
@@ -961,6 +990,7 @@ hipError_t launch_msm_prep28(int sig_g2, size_t n, uint8_t* status, const uint32
 // 256-thread blocks (the row tree's LDS buffer is sized for 256 lanes: one 64-lane block per CU would cap the many-row
 // launches at 256 waves).
 static unsigned few_waves_block(size_t nthreads) { return nthreads <= 256 * 64 ? 64u : 256u; }
+constexpr size_t FEW_THREADS = 1024 * 64;  // one wave per SIMD of the chip
 
 // nsets = 2: the sigma points S and the hash points Q share the sorted lists (the batch check); 1: S only
 template <class C>
@@ -985,11 +1015,23 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     }
   }
   const size_t rows = ngroups * g.nwin, ngw = (size_t)nsets * rows;
-  const unsigned sb = few_waves_block(ngw * g.nseg);
-  hipLaunchKernelGGL(k_msm_segsum28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs,
-                     ws.runs);
-  if (g.nseg > 1)
-    hipLaunchKernelGGL(k_msm_segoff28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, g, ngw, ws.segs, ws.runs);
+  // launches of at most one wave per SIMD (level 0's rows: 8 x 4,096 segment threads at 1M rounds) of the G1 kernels
+  // take the instantiation compiled for one wave per SIMD in 64-thread blocks: the whole register file, where the
+  // two-wave build spills (segment sums 292, offsets 228, row tree 128 B/lane)
+  const bool few = C::OCC > 1 && ngw * g.nseg <= FEW_THREADS;
+  const unsigned sb = few ? 64u : few_waves_block(ngw * g.nseg);
+  if (few)
+    hipLaunchKernelGGL((k_msm_segsum28<C, true>), dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, ws.buckets, ws.off, g, ngw, rows,
+                       ws.segs, ws.runs);
+  else
+    hipLaunchKernelGGL(k_msm_segsum28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs,
+                       ws.runs);
+  if (g.nseg > 1) {
+    if (few)
+      hipLaunchKernelGGL((k_msm_segoff28<C, true>), dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, g, ngw, ws.segs, ws.runs);
+    else
+      hipLaunchKernelGGL(k_msm_segoff28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, g, ngw, ws.segs, ws.runs);
+  }
   // row sums: ws.runs (free after the offsets) when a row's lanes fit one wave; else the waves' partials go to ws.runs
   // and the row sums to ws.segs
   // G: 8 when the rows' segments are many (the additions' count matters: the bisection's and the tbls per-signer
@@ -1006,9 +1048,15 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     lpr = (lpr + 63) / 64 * 64;
   }
   const uint32_t* rowsum = ws.runs;
-  if (g.nseg > 1)
-    hipLaunchKernelGGL(k_msm_rowtree28<C>, dim3(nblk(ngw * lpr, few_waves_block(ngw * lpr))), dim3(few_waves_block(ngw * lpr)), 0,
-                       st, ws.segs, g.nseg, G, ngw, lpr, span, ws.runs);
+  if (g.nseg > 1) {
+    const bool few_t = C::OCC > 1 && ngw * lpr <= FEW_THREADS;
+    const unsigned tb = few_t ? 64u : few_waves_block(ngw * lpr);
+    if (few_t)
+      hipLaunchKernelGGL((k_msm_rowtree28<C, true>), dim3(nblk(ngw * lpr, tb)), dim3(tb), 0, st, ws.segs, g.nseg, G, ngw, lpr, span,
+                         ws.runs);
+    else
+      hipLaunchKernelGGL(k_msm_rowtree28<C>, dim3(nblk(ngw * lpr, tb)), dim3(tb), 0, st, ws.segs, g.nseg, G, ngw, lpr, span, ws.runs);
+  }
   else
     rowsum = ws.segs;  // one segment per row: its value is the row sum
   if (lpr > 64) {
