@@ -858,8 +858,8 @@ DH_DEV typename C::P wave_tree(typename C::P acc, uint32_t* buf, uint32_t span) 
   return acc;
 }
 
-template <class C, bool FEW = false>
-__global__ __launch_bounds__(FEW ? 64 : 256, FEW ? 1 : C::OCC) void k_msm_segsum28(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ off,
+template <class C>
+__global__ __launch_bounds__(256, C::OCC) void k_msm_segsum28(const uint32_t* __restrict__ buckets, const uint32_t* __restrict__ off,
                                                               msm_geom g, size_t ngw, size_t rows_per_set, uint32_t* __restrict__ segs,
                                                               uint32_t* __restrict__ runs) {
   const size_t t = gtid();
@@ -889,8 +889,8 @@ DH_DEV typename C::P seg_off(const uint32_t* __restrict__ run, uint32_t k, const
   }
   return C::template add_mem<EXACT>(acc, tot);
 }
-template <class C, bool FEW = false>
-__global__ __launch_bounds__(FEW ? 64 : 256, FEW ? 1 : C::OCC) void k_msm_segoff28(msm_geom g, size_t ngw, uint32_t* __restrict__ segs,
+template <class C>
+__global__ __launch_bounds__(256, C::OCC) void k_msm_segoff28(msm_geom g, size_t ngw, uint32_t* __restrict__ segs,
                                                               const uint32_t* __restrict__ runs) {
   const size_t t = gtid();
   if (t >= ngw * g.nseg) return;
@@ -913,8 +913,8 @@ __global__ __launch_bounds__(FEW ? 64 : 256, FEW ? 1 : C::OCC) void k_msm_segoff
 // row sum in its first lane, or, for more than 64 lanes (a multiple of 64: fit_segments), one partial per wave that
 // k_msm_rowred28 (one wave per row) sums the same way. Measured against r04's launch tree on the tbls MSMs (64 groups of
 // 2 windows of 2,048 segments, gpurun_out r05w): the pure wave tree was 8.2 ms against 4.4.
-template <class C, bool FEW = false>
-__global__ __launch_bounds__(FEW ? 64 : 256, FEW ? 1 : C::OCC) void k_msm_rowtree28(const uint32_t* __restrict__ segs, uint32_t nseg, uint32_t G,
+template <class C>
+__global__ __launch_bounds__(256, C::OCC) void k_msm_rowtree28(const uint32_t* __restrict__ segs, uint32_t nseg, uint32_t G,
                                                                size_t ngw, uint32_t lpr, uint32_t span, uint32_t* __restrict__ out) {
   __shared__ uint32_t buf[lds_words<C>() * 256];
   const size_t t = gtid();
@@ -990,7 +990,6 @@ hipError_t launch_msm_prep28(int sig_g2, size_t n, uint8_t* status, const uint32
 // 256-thread blocks (the row tree's LDS buffer is sized for 256 lanes: one 64-lane block per CU would cap the many-row
 // launches at 256 waves).
 static unsigned few_waves_block(size_t nthreads) { return nthreads <= 256 * 64 ? 64u : 256u; }
-constexpr size_t FEW_THREADS = 1024 * 64;  // one wave per SIMD of the chip
 
 // nsets = 2: the sigma points S and the hash points Q share the sorted lists (the batch check); 1: S only
 template <class C>
@@ -1015,23 +1014,11 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     }
   }
   const size_t rows = ngroups * g.nwin, ngw = (size_t)nsets * rows;
-  // launches of at most one wave per SIMD (level 0's rows: 8 x 4,096 segment threads at 1M rounds) of the G1 kernels
-  // take the instantiation compiled for one wave per SIMD in 64-thread blocks: the whole register file, where the
-  // two-wave build spills (segment sums 292, offsets 228, row tree 128 B/lane)
-  const bool few = C::OCC > 1 && ngw * g.nseg <= FEW_THREADS;
-  const unsigned sb = few ? 64u : few_waves_block(ngw * g.nseg);
-  if (few)
-    hipLaunchKernelGGL((k_msm_segsum28<C, true>), dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, ws.buckets, ws.off, g, ngw, rows,
-                       ws.segs, ws.runs);
-  else
-    hipLaunchKernelGGL(k_msm_segsum28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs,
-                       ws.runs);
-  if (g.nseg > 1) {
-    if (few)
-      hipLaunchKernelGGL((k_msm_segoff28<C, true>), dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, g, ngw, ws.segs, ws.runs);
-    else
-      hipLaunchKernelGGL(k_msm_segoff28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, g, ngw, ws.segs, ws.runs);
-  }
+  const unsigned sb = few_waves_block(ngw * g.nseg);
+  hipLaunchKernelGGL(k_msm_segsum28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, ws.buckets, ws.off, g, ngw, rows, ws.segs,
+                     ws.runs);
+  if (g.nseg > 1)
+    hipLaunchKernelGGL(k_msm_segoff28<C>, dim3(nblk(ngw * g.nseg, sb)), dim3(sb), 0, st, g, ngw, ws.segs, ws.runs);
   // row sums: ws.runs (free after the offsets) when a row's lanes fit one wave; else the waves' partials go to ws.runs
   // and the row sums to ws.segs
   // G: 8 when the rows' segments are many (the additions' count matters: the bisection's and the tbls per-signer
@@ -1048,15 +1035,9 @@ static hipError_t msm28(const msm_geom& g, size_t ngroups, const uint32_t* S, co
     lpr = (lpr + 63) / 64 * 64;
   }
   const uint32_t* rowsum = ws.runs;
-  if (g.nseg > 1) {
-    const bool few_t = C::OCC > 1 && ngw * lpr <= FEW_THREADS;
-    const unsigned tb = few_t ? 64u : few_waves_block(ngw * lpr);
-    if (few_t)
-      hipLaunchKernelGGL((k_msm_rowtree28<C, true>), dim3(nblk(ngw * lpr, tb)), dim3(tb), 0, st, ws.segs, g.nseg, G, ngw, lpr, span,
-                         ws.runs);
-    else
-      hipLaunchKernelGGL(k_msm_rowtree28<C>, dim3(nblk(ngw * lpr, tb)), dim3(tb), 0, st, ws.segs, g.nseg, G, ngw, lpr, span, ws.runs);
-  }
+  if (g.nseg > 1)
+    hipLaunchKernelGGL(k_msm_rowtree28<C>, dim3(nblk(ngw * lpr, few_waves_block(ngw * lpr))), dim3(few_waves_block(ngw * lpr)), 0,
+                       st, ws.segs, g.nseg, G, ngw, lpr, span, ws.runs);
   else
     rowsum = ws.segs;  // one segment per row: its value is the row sum
   if (lpr > 64) {
