@@ -12,6 +12,7 @@
 #include <stdint.h>
 #include "consts.hpp"
 #include "fp_mul28.hpp"
+#include "inv_bingcd.hpp"
 
 namespace dh {
 
@@ -392,97 +393,15 @@ DH_DEV fp fp_pow_sched(const fp& x0, const uint32_t* sched, int len) {
 DH_DEV fp fp_inv(const fp& x) { return fp_pow_sched(x, cst::SCHED_INV, cst::SCHED_INV_LEN); }
 
 // Inversion of a PUBLIC element in variable time (verification data only — signatures, hash points, RLC sums; the
-// signing helpers keep the fixed exponentiation above). Binary extended Euclid on the integers with invariants
-// x1 a = u, x2 a = v (mod p); a run of k trailing zeros is removed at once, the matching division of x by 2^k is a
-// Montgomery-style halving x + m p with m = -x p^-1 mod 2^k. a = yR gives a^-1 = y^-1 R^-1, and one product by
-// R^3 mod p returns the Montgomery form y^-1 R. About 400 iterations of ~120 VALU ops: ~5x fewer than the
-// 455-product exponentiation, which sat on the latency path of every pairing check's affine conversion.
-DH_DEV void inv_vt_halve(uint32_t x[12], int k) {
-  const uint32_t m = (x[0] * DH_NP0) & ((1u << k) - 1u);
-  uint32_t t[13];
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    c += (uint64_t)m * p_limb(i) + x[i];
-    t[i] = (uint32_t)c;
-    c >>= 32;
-  }
-  t[12] = (uint32_t)c;
-#pragma unroll
-  for (int i = 0; i < 12; i++) x[i] = __builtin_amdgcn_alignbit(t[i + 1], t[i], k);
-  fp r;  // < 2p
-#pragma unroll
-  for (int i = 0; i < 12; i++) r.v[i] = x[i];
-  fp_reduce_once(r);
-#pragma unroll
-  for (int i = 0; i < 12; i++) x[i] = r.v[i];
-}
-DH_DEV void inv_vt_subx(uint32_t a[12], const uint32_t b[12]) {  // a = a - b mod p
-  unsigned br = 0, c = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) a[i] = __builtin_subc(a[i], b[i], br, &br);
-  const uint32_t mask = 0u - br;
-#pragma unroll
-  for (int i = 0; i < 12; i++) a[i] = __builtin_addc(a[i], p_limb(i) & mask, c, &c);
-}
-DH_DEV bool inv_vt_is_one(const uint32_t u[12]) {
-  uint32_t z = u[0] ^ 1u;
-#pragma unroll
-  for (int i = 1; i < 12; i++) z |= u[i];
-  return z == 0;
-}
+// signing helpers keep the fixed exponentiation above): inv_bingcd.hpp, Pornin's optimized binary GCD (25 rounds of
+// 31 divsteps on 64-bit approximations, the 12-word linear combinations once per round). It replaced (r06) a binary
+// extended Euclid with multi-bit halving, ~450 iterations of ~100 dependent VALU ops each (0.19 ms on one lane: the
+// pairing VM's inversion phase was 7% of a check, and every one-lane affine conversion and the MSM point prep's
+// per-workgroup inversion waited on it). a = yR gives a^-1 = y^-1 R^-1, and one product by R^3 mod p returns the
+// Montgomery form y^-1 R.
 // in place: a (integer in [1, p)) -> a^-1 mod p
-DH_DEV void inv_vt_int(uint32_t a[12]) {
-  uint32_t u[12], v[12], x1[12], x2[12];
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    u[i] = a[i];
-    v[i] = p_limb(i);
-    x1[i] = i == 0;
-    x2[i] = 0;
-  }
-  bool in_u = true;  // which of u, v reached 1
-#pragma unroll 1
-  while (true) {
-#pragma unroll 1
-    while ((u[0] & 1u) == 0) {
-      const int k = u[0] ? __builtin_ctz(u[0]) : 31;
-#pragma unroll
-      for (int i = 0; i < 11; i++) u[i] = __builtin_amdgcn_alignbit(u[i + 1], u[i], k);
-      u[11] >>= k;
-      inv_vt_halve(x1, k);
-    }
-    if (inv_vt_is_one(u)) break;
-    uint32_t d[12];
-    unsigned br = 0;
-#pragma unroll
-    for (int i = 0; i < 12; i++) d[i] = __builtin_subc(u[i], v[i], br, &br);
-    if (!br) {  // u > v (u == v only at u = v = 1, caught above)
-#pragma unroll
-      for (int i = 0; i < 12; i++) u[i] = d[i];
-      inv_vt_subx(x1, x2);
-    } else {  // v - u = -d, even
-      unsigned b2 = 0;
-#pragma unroll
-      for (int i = 0; i < 12; i++) v[i] = __builtin_subc(0u, d[i], b2, &b2);
-      inv_vt_subx(x2, x1);
-#pragma unroll 1
-      while ((v[0] & 1u) == 0) {
-        const int k = v[0] ? __builtin_ctz(v[0]) : 31;
-#pragma unroll
-        for (int i = 0; i < 11; i++) v[i] = __builtin_amdgcn_alignbit(v[i + 1], v[i], k);
-        v[11] >>= k;
-        inv_vt_halve(x2, k);
-      }
-      if (inv_vt_is_one(v)) {
-        in_u = false;
-        break;
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 12; i++) a[i] = in_u ? x1[i] : x2[i];
-}
+DH_DEV void inv_vt_int(uint32_t a[12]) { bgcd::inverse(a); }
+
 DH_DEV fp fp_inv_vt(const fp& a) {
   if (fp_is_zero(a)) return a;
   fp r = a;
